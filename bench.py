@@ -1,0 +1,218 @@
+"""bench.py -- env-steps/s of the batched 1024x1024x24 hologram VecEnv on MI355X.
+
+Workload (BASELINE.json configs[2]; configs[3] at --gpus 8): 128 independent
+environments per GPU, each a 1024x1024 mask of 24 binary planes (3 colour
+groups x 8 time-multiplexed planes, 638/515/450 nm, 7.56 um pitch, z = 2 mm),
+stepped with one action per env per VecEnv step.  One env-step = decode ->
+flip -> re-propagate the touched colour group (8 planes, 2-D FFT ASM) ->
+|.|^2 plane mean -> relative PSNR -> reward / accept-rollback / termination
+(env.py:154-259; DBS_1024_24.py:313-422).  Synthetic data:
+pre_model ~ U[0,1) -> mask = pre >= 0.5, target ~ U[0,1), actions ~ U{0..CH*N^2-1}.
+
+N GPUs: one process per GPU (torchrun), 128 envs per rank (weak scaling), the
+per-step rewards / psnr / done flags gathered to rank 0 over RCCL.
+
+Prints ONE JSON line on rank 0 (driver contract), plus `roofline` for the
+dominant kernel (live hipEvent timing) and `cpu_baseline` (the float64
+numpy oracle timed on this host, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "binary-hologram-reinforcement-learning_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--envs", type=int, default=128, help="envs per GPU")
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--cpu-sample", type=int, default=12,
+                    help="env-steps of the numpy oracle timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--no-psnr-check", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(N: int, P: int):
+    """HBM bytes each pass must move per job (one colour group of one env):
+    k_rowfwd: read P*N^2/8 mask bits, write P*N^2/2 complex64 (half spectrum)
+    k_col:    read P*N^2/2 complex64, write P*N^2 complex64
+    k_rowinv: read P*N^2 complex64 + N^2 f32 target."""
+    return {"k_rowfwd": P * N * N // 8 + P * N * N * 4,
+            "k_col": P * N * N * 4 + P * N * N * 8,
+            "k_rowinv": P * N * N * 8 + N * N * 4}
+
+
+def cpu_baseline(n_steps: int, N: int):
+    """numpy float64 oracle env-step (one 8-plane group propagate + PSNR + reward), 1 core."""
+    import numpy as np
+    from oracle import hbx_oracle as O
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    cfg = O.rgb_config(N)
+    pre, tgt = O.synthetic_inputs(cfg, 0)
+    env = O.OracleEnv(cfg)
+    env.reset(pre, tgt)
+    acts = np.random.default_rng(2).integers(0, cfg.channels * N * N, n_steps + 2)
+    env.step(int(acts[0]))      # warm-up (2 steps: SURVEY 8d)
+    env.step(int(acts[1]))
+    t0 = time.perf_counter()
+    for a in acts[2:]:
+        env.step(int(a))
+    dt = time.perf_counter() - t0
+    return {"value": n_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_steps} env-steps of the {N}x{N}x24 RGB env (one 8-plane group propagate each), "
+                      f"numpy.fft complex128 oracle (oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
+
+
+def psnr_check(vec, N):
+    """PSNR delta vs the numpy oracle for env 0's initial state (full 24-plane propagate)."""
+    import numpy as np
+    from oracle import hbx_oracle as O
+    cfg = O.rgb_config(N)
+    mask = vec.state.mask[0].cpu().numpy().view("<u8")
+    m = O.unpack_mask(mask, N)
+    tgt = vec.state.target[0].cpu().numpy()
+    prop = O.Propagator(cfg)
+    inten = prop.all_intensity(m)
+    st = np.stack([O.chan_stats(inten[g], tgt[g]) for g in range(3)])
+    return abs(prop.psnr(st) - float(vec.state.init_psnr[0].item()))
+
+
+def load_pmc_traffic():
+    """Per-launch HBM bytes of the dominant kernels from the committed rocprofv3
+    PMC summary (profiles/pmc_latest.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 read correction)."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p))
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    from hbx import dist as hd
+    from hbx.env import HologramVecEnv
+    from hbx.plan import rgb_config
+
+    rank, world, local = hd.init()
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    N, B = args.size, args.envs
+    cfg = rgb_config(N)
+    CH, G, P = cfg.channels, cfg.groups, cfg.planes
+
+    # synthetic, seeded per global env index
+    def target_source(i):
+        g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i) + 1)
+        return torch.rand((G, N, N), generator=g, device="cuda")
+
+    def pre_model_source(i):
+        g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i))
+        return torch.rand((CH, N, N), generator=g, device="cuda")
+
+    vec = HologramVecEnv(cfg, B, target_source, pre_model_source=pre_model_source, obs_keys=(),
+                         auto_reset=False, max_steps=10 ** 9)
+    vec.reset()
+    gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
+    n_act = CH * N * N
+    total_steps = args.warmup + args.steps
+    actions = torch.randint(0, n_act, (total_steps, B), generator=gen, device="cuda", dtype=torch.int64)
+    gather = (world > 1) and not args.no_gather
+
+    def one_step(k):
+        r, ps, acc, term, trunc = vec.step_device(actions[k])
+        if gather:
+            hd.gather_to_rank0(hd.pack_step_metrics(r, ps, acc, term, trunc))
+
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize()
+    vec.plan.set_timing(args.steps + 1)
+    hd.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total_steps):
+        one_step(k)
+    torch.cuda.synchronize()
+    hd.barrier()
+    dt_local = time.perf_counter() - t0
+    dt = hd.max_over_ranks(dt_local, torch.device("cuda", local))
+    timing = vec.plan.read_timing()
+    vec.state.check_error()
+
+    env_steps = B * world * args.steps
+    value = env_steps / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    if rank != 0:
+        return
+    abytes = algorithmic_bytes(N, P)
+    passes = {}
+    for name, (ms, launches, jobs) in timing.items():
+        if launches:
+            avg = ms / launches
+            per_launch = abytes[name] * (jobs / launches)
+            passes[name] = {"avg_ms": avg, "launches": launches, "jobs_per_launch": jobs / launches,
+                            "alg_bytes_per_launch": per_launch,
+                            "achieved_GBs": per_launch / (avg * 1e-3) / 1e9}
+    dom = max(passes, key=lambda n: passes[n]["avg_ms"])
+    d = passes[dom]
+    pmc = load_pmc_traffic()
+    traffic = None
+    if pmc and dom in pmc.get("kernels", {}):
+        kinfo = pmc["kernels"][dom]
+        if kinfo.get("jobs_per_launch") == d["jobs_per_launch"] and kinfo.get("N") == N:
+            traffic = kinfo.get("hbm_bytes_per_launch")
+    roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
+    step_bytes = sum(abytes.values()) * B
+    out = {
+        "metric": "env-steps/sec (1024x1024, 24-plane)",
+        "value": round(value, 2),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded U[0,1) pre-model/targets, uniform actions)",
+        "config": {"workload": "configs[2]: batched VecEnv.step, 128 envs/GPU x 1024x1024x24-plane "
+                               "(3 colour groups x 8 planes), one action per env per step",
+                   "envs_per_gpu": B, "global_envs": B * world, "size": N, "planes": CH,
+                   "parallelism": f"env-sharded x{world}" + (" + RCCL metric gather" if gather else "")},
+        "roofline": roofline,
+        "passes": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                   for k, v in passes.items()},
+        "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+    }
+    if world == 1 and not args.no_psnr_check:
+        out["psnr_delta_vs_numpy"] = psnr_check(vec, N)
+    if world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, N)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

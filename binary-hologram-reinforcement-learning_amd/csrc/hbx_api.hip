@@ -1,0 +1,483 @@
+// hbx_api.hip -- the extern "C" boundary declared in include/hbx.h.
+//
+// Plans own twiddle / transfer-function tables (built once in float64 on the
+// host) and a per-job workspace.  Entry points only enqueue work on the given
+// stream: no allocation, copy or synchronisation happens inside a launch
+// function after the plan exists, so callers may capture them in hipGraphs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "hbx.h"
+#include "hbx_internal.hpp"
+
+using hbx::EnvDev;
+using hbx::EnvParams;
+using hbx::JobDesc;
+using hbx::PlanDev;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HBX_HIP(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(HBX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+}  // namespace
+
+struct hbx_plan {
+  hbx_optics_t optics;
+  PlanDev pd;
+  int device;
+  int max_jobs;
+  size_t ws_bytes;
+  JobDesc* jobs;          // [max_jobs]
+  float* job_inten;       // [max_jobs][N][N]
+  int32_t* accept_flag;   // [max_jobs]
+  int32_t* err;           // [1]
+};
+
+namespace {
+
+int check_plan(hbx_plan_t p) {
+  if (!p) return fail(HBX_ERR_INVALID, "null plan");
+  return HBX_OK;
+}
+
+double fftfreq(int k, int n, double d) {
+  const int kk = (k < (n + 1) / 2) ? k : k - n;  // numpy.fft.fftfreq ordering
+  return (double)kk / ((double)n * d);
+}
+
+std::complex<double> transfer(const hbx_optics_t& o, double wl, double fx, double fy) {
+  const double f2 = fx * fx + fy * fy;
+  if (o.tf_kind == HBX_TF_ASM) {
+    const double arg = 1.0 / (wl * wl) - f2;
+    if (arg <= 0.0) return {0.0, 0.0};
+    // |U|^2 is blind to the global phase 2 pi z / wl; keep it anyway (double).
+    const double ph = 2.0 * M_PI * o.z * std::sqrt(arg);
+    return {std::cos(ph), std::sin(ph)};
+  }
+  const double ph = 2.0 * M_PI * o.z / wl - M_PI * wl * o.z * f2;
+  return {std::cos(ph), std::sin(ph)};
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbx_abi_version(void) { return HBX_ABI_VERSION; }
+
+const char* hbx_last_error(void) { return g_last_error.c_str(); }
+
+int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, int32_t device) {
+  if (!out || !o) return fail(HBX_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (o->height != o->width) return fail(HBX_ERR_UNSUPPORTED, "only square N x N masks are built");
+  int R = 0;
+  if (o->height == 1024) R = 32;
+  else if (o->height == 256) R = 16;
+  else if (o->height == 64) R = 8;
+  else return fail(HBX_ERR_UNSUPPORTED, "N must be 64, 256 or 1024");
+  if (o->groups < 1 || o->groups > HBX_MAX_GROUPS) return fail(HBX_ERR_INVALID, "groups out of range");
+  if (o->planes < 2 || (o->planes % 2)) return fail(HBX_ERR_INVALID, "planes must be even and >= 2");
+  if (max_jobs < o->groups) return fail(HBX_ERR_INVALID, "max_jobs must be >= groups");
+  if (o->tf_kind != HBX_TF_ASM && o->tf_kind != HBX_TF_FRESNEL) return fail(HBX_ERR_INVALID, "tf_kind");
+  if (o->field_kind != HBX_FIELD_AMPLITUDE && o->field_kind != HBX_FIELD_PHASE)
+    return fail(HBX_ERR_INVALID, "field_kind");
+  if (o->rel_scale != HBX_REL_NONE && o->rel_scale != HBX_REL_LSQ) return fail(HBX_ERR_INVALID, "rel_scale");
+  for (int g = 0; g < o->groups; ++g)
+    if (!(o->wavelength[g] > 0.0)) return fail(HBX_ERR_INVALID, "wavelength must be > 0");
+  if (!(o->dx > 0.0) || !(o->dy > 0.0)) return fail(HBX_ERR_INVALID, "pixel pitch must be > 0");
+
+  HBX_HIP(hipSetDevice(device));
+  hbx_plan* p = new (std::nothrow) hbx_plan();
+  if (!p) return fail(HBX_ERR_NOMEM, "host allocation");
+  std::memset(p, 0, sizeof(*p));
+  p->optics = *o;
+  p->device = device;
+  p->max_jobs = max_jobs;
+  const int N = o->height, G = o->groups, P = o->planes;
+  PlanDev& pd = p->pd;
+  pd.R = R; pd.N = N; pd.G = G; pd.P = P;
+  if (o->field_kind == HBX_FIELD_AMPLITUDE) { pd.va = 0.0f; pd.vb = 1.0f; }
+  else { pd.va = 1.0f; pd.vb = -2.0f; }
+
+  // host tables in float64, rounded once to complex64
+  std::vector<float2> tw((size_t)N);
+  for (int k1 = 0; k1 < R; ++k1)
+    for (int t = 0; t < R; ++t) {
+      const double a = -2.0 * M_PI * (double)((t * k1) % N) / (double)N;
+      tw[(size_t)k1 * R + t] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+  const size_t hrow = (size_t)(N / 2 + 1) * N;
+  std::vector<float2> ht((size_t)G * hrow);
+  const double scale = 1.0 / ((double)N * (double)N);  // ifft2 normalisation
+  for (int g = 0; g < G; ++g)
+    for (int kx = 0; kx <= N / 2; ++kx) {
+      const double fx = fftfreq(kx, N, o->dx);
+      for (int ky = 0; ky < N; ++ky) {
+        const double fy = fftfreq(ky, N, o->dy);
+        const std::complex<double> h = transfer(*o, o->wavelength[g], fx, fy) * scale;
+        ht[g * hrow + (size_t)kx * N + ky] = make_float2((float)h.real(), (float)h.imag());
+      }
+    }
+  const int RB = N / (256 / R);
+  p->ws_bytes = (size_t)max_jobs * P * N * N * sizeof(float2);
+  auto cleanup = [&](int code, const std::string& msg) {
+    hbx_plan_destroy(p);
+    return fail(code, msg);
+  };
+  if (hipMalloc(&pd.tw, tw.size() * sizeof(float2)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "tw");
+  if (hipMalloc(&pd.htab, ht.size() * sizeof(float2)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "htab");
+  if (hipMalloc(&pd.ws, p->ws_bytes) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "workspace");
+  if (hipMalloc(&pd.partial, (size_t)max_jobs * RB * 3 * sizeof(double)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "partial");
+  if (hipMalloc(&pd.job_stats, (size_t)max_jobs * 3 * sizeof(double)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "job_stats");
+  if (hipMalloc(&p->jobs, (size_t)max_jobs * sizeof(JobDesc)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "jobs");
+  if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "accept_flag");
+  if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
+  if (hipMemcpy(pd.tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess)
+    return cleanup(HBX_ERR_HIP, "table upload");
+  size_t lds = 0;
+  if (hbx::col_kernel_lds(R, &lds) != hipSuccess) return cleanup(HBX_ERR_HIP, "column kernel LDS attribute");
+  *out = p;
+  return HBX_OK;
+}
+
+int hbx_plan_destroy(hbx_plan_t p) {
+  if (!p) return HBX_OK;
+  (void)hipSetDevice(p->device);
+  if (p->pd.tw) (void)hipFree(p->pd.tw);
+  if (p->pd.htab) (void)hipFree(p->pd.htab);
+  if (p->pd.ws) (void)hipFree(p->pd.ws);
+  if (p->pd.partial) (void)hipFree(p->pd.partial);
+  if (p->pd.job_stats) (void)hipFree(p->pd.job_stats);
+  if (p->jobs) (void)hipFree(p->jobs);
+  if (p->job_inten) (void)hipFree(p->job_inten);
+  if (p->accept_flag) (void)hipFree(p->accept_flag);
+  if (p->err) (void)hipFree(p->err);
+  hbx_plan_set_timing(p, 0);
+  delete p;
+  return HBX_OK;
+}
+
+size_t hbx_plan_workspace_bytes(hbx_plan_t p) { return p ? p->ws_bytes : 0; }
+
+}  // extern "C"
+
+namespace {
+
+int ensure_job_inten(hbx_plan_t p) {
+  if (p->job_inten) return HBX_OK;
+  const size_t bytes = (size_t)p->max_jobs * p->pd.N * p->pd.N * sizeof(float);
+  if (hipMalloc(&p->job_inten, bytes) != hipSuccess) return fail(HBX_ERR_NOMEM, "job intensity buffer");
+  return HBX_OK;
+}
+
+double pixel_count(const hbx_plan_t p) {
+  return (double)p->pd.G * (double)p->pd.N * (double)p->pd.N;
+}
+
+EnvDev env_dev(const hbx_env_buffers_t* e) {
+  EnvDev d;
+  d.mask = e->mask; d.record = e->record; d.target = e->target; d.chan_stats = e->chan_stats;
+  d.init_psnr = e->init_psnr; d.prev_psnr = e->prev_psnr; d.max_psnr_diff = e->max_psnr_diff;
+  d.steps = e->steps; d.flip_count = e->flip_count; d.sustained = e->sustained;
+  return d;
+}
+
+EnvDev env_offset(const EnvDev& d, size_t e0, int CH, int G, int N) {
+  EnvDev o = d;
+  const size_t mwords = (size_t)CH * N * (N / 64);
+  o.mask = d.mask + e0 * mwords;
+  o.record = d.record ? d.record + e0 * (size_t)CH * N * N : nullptr;
+  o.target = d.target + e0 * (size_t)G * N * N;
+  o.chan_stats = d.chan_stats + e0 * G * 3;
+  o.init_psnr = d.init_psnr + e0;
+  o.prev_psnr = d.prev_psnr + e0;
+  o.max_psnr_diff = d.max_psnr_diff + e0;
+  o.steps = d.steps + e0;
+  o.flip_count = d.flip_count + e0;
+  o.sustained = d.sustained + e0;
+  return o;
+}
+
+// full propagation of n_ids envs (absolute ids from env_ids, or 0..n_ids-1)
+int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, const int32_t* env_ids,
+                   int n_ids, float* intensity, double* chan_stats, double* psnr, const EnvDev* env,
+                   hipStream_t st) {
+  const PlanDev& pd = p->pd;
+  const int G = pd.G;
+  const int chunk = p->max_jobs / G;
+  if (intensity) {
+    int rc = ensure_job_inten(p);
+    if (rc) return rc;
+  }
+  EnvDev dummy;
+  std::memset(&dummy, 0, sizeof(dummy));
+  for (int i0 = 0; i0 < n_ids; i0 += chunk) {
+    const int n = std::min(chunk, n_ids - i0);
+    // with env_ids the jobs carry absolute env ids; without, ids are chunk-local
+    // and every per-env buffer is offset by i0 instead
+    HBX_HIP(hbx::launch_jobs_full(env_ids ? env_ids + i0 : nullptr, n, G, p->jobs, st));
+    const size_t mwords = (size_t)G * pd.P * pd.N * (pd.N / 64);
+    const uint64_t* m = env_ids ? mask : mask + (size_t)i0 * mwords;
+    const float* tg = env_ids ? target : target + (size_t)i0 * G * pd.N * pd.N;
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
+                          intensity ? p->job_inten : nullptr, st));
+    double* cs = env_ids ? chan_stats : chan_stats + (size_t)i0 * G * 3;
+    double* ps = psnr ? (env_ids ? psnr : psnr + i0) : nullptr;
+    EnvDev ed = dummy;
+    if (env) ed = env_ids ? *env : env_offset(*env, i0, G * pd.P, G, pd.N);
+    HBX_HIP(hbx::launch_full_finalize(p->jobs, pd.job_stats, n, G, cs, ps, pixel_count(p),
+                                      p->optics.rel_scale, p->optics.peak, ed, env ? 1 : 0, st));
+    if (intensity) {
+      float* cache = env_ids ? intensity : intensity + (size_t)i0 * G * pd.N * pd.N;
+      HBX_HIP(hbx::launch_scatter_intensity(p->jobs, n * G, p->job_inten, cache, G,
+                                            (size_t)pd.N * pd.N, nullptr, st));
+    }
+  }
+  return HBX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbx_propagate(hbx_plan_t p, const uint64_t* mask, const float* target, int32_t n_env,
+                  float* intensity, double* chan_stats, double* psnr, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!mask || !target || !chan_stats || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
+  if (n_env == 0) return HBX_OK;
+  HBX_HIP(hipSetDevice(p->device));
+  return propagate_full(p, mask, target, nullptr, n_env, intensity, chan_stats, psnr, nullptr,
+                        (hipStream_t)stream);
+}
+
+int hbx_psnr(hbx_plan_t p, const double* chan_stats, int32_t n_env, double* psnr, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!chan_stats || !psnr || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
+  if (n_env == 0) return HBX_OK;
+  HBX_HIP(hipSetDevice(p->device));
+  HBX_HIP(hbx::launch_psnr(chan_stats, n_env, p->pd.G, psnr, pixel_count(p), p->optics.rel_scale,
+                           p->optics.peak, (hipStream_t)stream));
+  return HBX_OK;
+}
+
+int hbx_env_reset(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const int32_t* env_ids,
+                  int32_t n_ids, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!e || !e->mask || !e->target || !e->chan_stats || !e->init_psnr || !e->prev_psnr ||
+      !e->max_psnr_diff || !e->steps || !e->flip_count || !e->sustained)
+    return fail(HBX_ERR_INVALID, "env buffers incomplete");
+  if (n_env < 0) return fail(HBX_ERR_INVALID, "n_env");
+  const int n = env_ids ? n_ids : n_env;
+  if (n <= 0) return HBX_OK;
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int CH = pd.G * pd.P;
+  if (e->record)
+    HBX_HIP(hbx::launch_zero_record(e->record, env_ids, n, (size_t)CH * pd.N * pd.N, st));
+  EnvDev ed = env_dev(e);
+  return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed, st);
+}
+
+int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_t* prm,
+                 int32_t n_env, const int64_t* actions, double* reward, double* psnr,
+                 uint8_t* accepted, uint8_t* terminated, uint8_t* truncated, float* group_intensity,
+                 void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!e || !prm || !actions || !e->mask || !e->target || !e->chan_stats || !e->init_psnr ||
+      !e->prev_psnr || !e->max_psnr_diff || !e->steps || !e->flip_count || !e->sustained)
+    return fail(HBX_ERR_INVALID, "env buffers incomplete");
+  if (prm->accept_rule != HBX_ACCEPT_ENV && prm->accept_rule != HBX_ACCEPT_DBS)
+    return fail(HBX_ERR_INVALID, "accept_rule");
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  const size_t hw = (size_t)N * N;
+  const bool want_inten = group_intensity || e->intensity;
+  if (want_inten) {
+    rc = ensure_job_inten(p);
+    if (rc) return rc;
+  }
+  EnvParams ep;
+  ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
+  ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
+  ep.accept_rule = prm->accept_rule;
+  const EnvDev base = env_dev(e);
+  for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, n_env - b0);
+    const EnvDev ed = env_offset(base, b0, CH, G, N);
+    HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,
+                          want_inten ? p->job_inten : nullptr, st));
+    HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),
+                                          p->optics.rel_scale, p->optics.peak,
+                                          reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
+                                          accepted ? accepted + b0 : nullptr,
+                                          terminated ? terminated + b0 : nullptr,
+                                          truncated ? truncated + b0 : nullptr, p->accept_flag, st));
+    if (group_intensity)
+      HBX_HIP(hipMemcpyAsync(group_intensity + (size_t)b0 * hw, p->job_inten, (size_t)n * hw * sizeof(float),
+                             hipMemcpyDeviceToDevice, st));
+    if (e->intensity)
+      HBX_HIP(hbx::launch_scatter_intensity(p->jobs, n, p->job_inten, e->intensity + (size_t)b0 * G * hw, G,
+                                            hw, p->accept_flag, st));
+  }
+  return HBX_OK;
+}
+
+int hbx_step(hbx_plan_t p, uint64_t* mask, const int64_t* actions, int32_t n_env, const float* target,
+             double* chan_stats, double* prev_psnr, double* psnr_out, uint8_t* accepted,
+             int32_t accept_rule, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!mask || !actions || !target || !chan_stats || !prev_psnr) return fail(HBX_ERR_INVALID, "null buffer");
+  if (accept_rule != HBX_ACCEPT_ENV && accept_rule != HBX_ACCEPT_DBS) return fail(HBX_ERR_INVALID, "accept_rule");
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, n_env - b0);
+    uint64_t* m = mask + (size_t)b0 * CH * N * (N / 64);
+    const float* tg = target + (size_t)b0 * G * N * N;
+    HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, p->err, st));
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(m), tg, nullptr, st));
+    HBX_HIP(hbx::launch_dbs_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, m,
+                                          chan_stats + (size_t)b0 * G * 3, prev_psnr + b0,
+                                          psnr_out ? psnr_out + b0 : nullptr,
+                                          accepted ? accepted + b0 : nullptr, accept_rule,
+                                          pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
+  }
+  return HBX_OK;
+}
+
+int hbx_eval_flips(hbx_plan_t p, const uint64_t* base_mask, const float* target,
+                   const double* base_chan_stats, const int64_t* flips, int32_t K, double* psnr_out,
+                   double* group_stats, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !target || !base_chan_stats || !flips || !psnr_out)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  for (int k0 = 0; k0 < K; k0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, K - k0);
+    HBX_HIP(hbx::launch_jobs_from_flips(flips + k0, n, N, N, P, CH, p->jobs, st));
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr, st));
+    HBX_HIP(hbx::launch_eval_finalize(p->jobs, pd.job_stats, n, G, base_chan_stats, psnr_out + k0,
+                                      group_stats ? group_stats + (size_t)k0 * 3 : nullptr,
+                                      pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
+  }
+  return HBX_OK;
+}
+
+int hbx_commit_flip(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, double* prev_psnr,
+                    const int64_t* flips, const double* psnr_out, const double* group_stats,
+                    const int32_t* k, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !base_chan_stats || !prev_psnr || !flips || !psnr_out || !group_stats || !k)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  HBX_HIP(hipSetDevice(p->device));
+  const PlanDev& pd = p->pd;
+  HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
+                                  0x7fffffff, pd.G, pd.P, pd.N, pd.N, (hipStream_t)stream));
+  return HBX_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (capacity < 0) return fail(HBX_ERR_INVALID, "capacity");
+  (void)hipSetDevice(p->device);
+  hbx::PassTimer* tm = p->pd.timer;
+  if (tm) {
+    for (int k = 0; k < 3; ++k) {
+      for (int i = 0; i < 2 * tm->capacity; ++i) (void)hipEventDestroy(tm->ev[k][i]);
+      delete[] tm->ev[k];
+    }
+    delete tm;
+    p->pd.timer = nullptr;
+  }
+  if (capacity == 0) return HBX_OK;
+  tm = new (std::nothrow) hbx::PassTimer();
+  if (!tm) return fail(HBX_ERR_NOMEM, "timer");
+  tm->capacity = capacity;
+  for (int k = 0; k < 3; ++k) {
+    tm->ev[k] = new (std::nothrow) hipEvent_t[2 * (size_t)capacity];
+    if (!tm->ev[k]) return fail(HBX_ERR_NOMEM, "timer events");
+    for (int i = 0; i < 2 * capacity; ++i) HBX_HIP(hipEventCreate(&tm->ev[k][i]));
+  }
+  p->pd.timer = tm;
+  return HBX_OK;
+}
+
+int hbx_plan_read_timing(hbx_plan_t p, double* ms_total, int64_t* launches, int64_t* jobs) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!ms_total || !launches) return fail(HBX_ERR_INVALID, "null output");
+  hbx::PassTimer* tm = p->pd.timer;
+  for (int k = 0; k < 3; ++k) {
+    ms_total[k] = 0.0;
+    launches[k] = 0;
+    if (jobs) jobs[k] = 0;
+  }
+  if (!tm) return fail(HBX_ERR_INVALID, "timing not enabled");
+  (void)hipSetDevice(p->device);
+  for (int k = 0; k < 3; ++k) {
+    double tot = 0.0;
+    for (int i = 0; i < tm->count[k]; ++i) {
+      HBX_HIP(hipEventSynchronize(tm->ev[k][2 * i + 1]));
+      float ms = 0.0f;
+      HBX_HIP(hipEventElapsedTime(&ms, tm->ev[k][2 * i], tm->ev[k][2 * i + 1]));
+      tot += ms;
+    }
+    ms_total[k] = tot;
+    launches[k] = tm->count[k];
+    if (jobs) jobs[k] = tm->jobs[k];
+    tm->count[k] = 0;
+    tm->jobs[k] = 0;
+  }
+  return HBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// hbx_internal.hpp -- types shared by the kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace hbx {
+
+// One colour-group propagation: env index (plan-local), group, optional flip.
+struct JobDesc {
+  int32_t env;         // < 0: invalid job (skipped, outputs neutral)
+  int32_t group;
+  int32_t flip_plane;  // plane within the group, -1 = no flip
+  int32_t flip_pix;    // row * W + col
+};
+
+// Optional hipEvent pairs around every pass launch (hbx_plan_set_timing).
+struct PassTimer {
+  int capacity = 0;
+  int count[3] = {0, 0, 0};
+  int64_t jobs[3] = {0, 0, 0};
+  hipEvent_t* ev[3] = {nullptr, nullptr, nullptr};  // [2 * capacity] start/stop
+  __host__ void begin(int pass, hipStream_t st) {
+    if (capacity && count[pass] < capacity) (void)hipEventRecord(ev[pass][2 * count[pass]], st);
+  }
+  __host__ void end(int pass, int n_jobs, hipStream_t st) {
+    if (capacity && count[pass] < capacity) {
+      (void)hipEventRecord(ev[pass][2 * count[pass] + 1], st);
+      ++count[pass];
+      jobs[pass] += n_jobs;
+    }
+  }
+};
+
+struct PlanDev {
+  int R;               // N = R * R
+  int N, G, P;
+  float va, vb;        // field = va + vb * bit
+  float2* tw;          // [N]  W_N^{t k1} at [k1 * R + t]
+  float2* htab;        // [G][N/2 + 1][N]  H(kx, ky) / N^2
+  float2* ws;          // [max_jobs][P][N][N]
+  double* partial;     // [max_jobs][N / (256/R)][3]
+  double* job_stats;   // [max_jobs][3]
+  PassTimer* timer;    // nullable
+};
+
+struct EnvDev {
+  uint64_t* mask;
+  int8_t* record;
+  const float* target;
+  double* chan_stats;
+  double* init_psnr;
+  double* prev_psnr;
+  double* max_psnr_diff;
+  int64_t* steps;
+  int64_t* flip_count;
+  int64_t* sustained;
+};
+
+struct EnvParams {
+  int64_t max_steps;
+  double t_psnr;
+  int64_t t_steps;
+  double t_psnr_diff;
+  double reward_weight;
+  int32_t accept_rule;
+};
+
+hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
+                    const float* target, float* inten_out, hipStream_t st);
+hipError_t col_kernel_lds(int R, size_t* bytes);
+hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W, int P, int CH,
+                                    JobDesc* jobs, int32_t* err, hipStream_t st);
+hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int P, int CH,
+                                  JobDesc* jobs, hipStream_t st);
+hipError_t launch_jobs_full(const int32_t* env_ids, int n_ids, int G, JobDesc* jobs, hipStream_t st);
+hipError_t launch_full_finalize(const JobDesc* jobs, const double* job_stats, int n_ids, int G,
+                                double* chan_stats, double* psnr, double count, int rel, double peak,
+                                const EnvDev& env, int reset, hipStream_t st);
+hipError_t launch_env_step_finalize(const JobDesc* jobs, const double* job_stats, int n, int G,
+                                    int P, int H, int W, const EnvDev& env, const EnvParams& prm,
+                                    double count, int rel, double peak, double* reward, double* psnr,
+                                    uint8_t* acc, uint8_t* term, uint8_t* trunc, int32_t* accept_flag,
+                                    hipStream_t st);
+hipError_t launch_dbs_step_finalize(const JobDesc* jobs, const double* job_stats, int n, int G, int P,
+                                    int H, int W, uint64_t* mask, double* chan_stats, double* prev,
+                                    double* psnr, uint8_t* acc, int rule, double count, int rel,
+                                    double peak, hipStream_t st);
+hipError_t launch_eval_finalize(const JobDesc* jobs, const double* job_stats, int K, int G,
+                                const double* base_stats, double* psnr, double* gstats, double count,
+                                int rel, double peak, hipStream_t st);
+hipError_t launch_commit_flip(uint64_t* mask, double* stats, double* prev, const int64_t* flips,
+                              const double* psnr, const double* gstats, const int32_t* k, int K,
+                              int G, int P, int H, int W, hipStream_t st);
+hipError_t launch_zero_record(int8_t* record, const int32_t* env_ids, int n_ids, size_t per_env,
+                              hipStream_t st);
+hipError_t launch_scatter_intensity(const JobDesc* jobs, int n_jobs, const float* src, float* cache,
+                                    int G, size_t hw, const int32_t* accept_flag, hipStream_t st);
+hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, double count, int rel,
+                       double peak, hipStream_t st);
+
+}  // namespace hbx

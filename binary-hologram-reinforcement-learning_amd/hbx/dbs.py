@@ -1,0 +1,149 @@
+"""Direct binary search drivers on the device.
+
+greedy()  -- DBS.py:247-294 / DBS_1024_24.py:313-422: visit pixels in a
+             shuffled order, keep a flip iff PSNR strictly improves.  Run as
+             SPECULATIVE batches: the next K candidates are evaluated against
+             the current base in one hbx_eval_flips launch; the first improving
+             one (in visiting order) is committed on the device and the walk
+             resumes right after it.  Every candidate before it was evaluated
+             against exactly the state the serial loop would have had, so the
+             accept sequence is the serial one.
+probe()   -- DBS_1024_24-128.py:310-373 / range.py:294-335: every flip
+             evaluated against the FIXED base and undone; embarrassingly
+             parallel, one launch per max_jobs candidates.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .plan import Plan
+
+OUTPUT_BINS = np.round(np.linspace(0, 1.0, 11), decimals=10)   # DBS_1024_24.py:209
+
+
+@dataclass
+class GreedyResult:
+    initial_psnr: float
+    final_psnr: float
+    steps: int                       # candidates visited (serial-loop `steps`)
+    accepted_positions: List[int]    # positions in `order` that were accepted
+    accepted_psnr: List[float]
+    launches: int
+    stopped_early: bool = False
+
+
+class KController:
+    """Adaptive speculation depth: short batches while flips are often
+    accepted, long ones once acceptance becomes rare."""
+
+    def __init__(self, k_min: int = 4, k_max: int = 256, k0: int = 16):
+        self.k_min, self.k_max, self.k = k_min, k_max, k0
+
+    def update(self, found_at: Optional[int]):
+        if found_at is None:
+            self.k = min(self.k_max, self.k * 2)
+        else:
+            self.k = int(min(self.k_max, max(self.k_min, 2 * (found_at + 1))))
+        return self.k
+
+
+def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
+    """Index of the first candidate with psnr > prev (strict, DBS_1024_24.py:355)."""
+    idx = np.nonzero(psnr > prev)[0]
+    return int(idx[0]) if idx.size else None
+
+
+def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
+           k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
+           stream=None) -> GreedyResult:
+    """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32."""
+    dev = plan.device
+    k_max = min(k_max or plan.max_jobs, plan.max_jobs)
+    order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
+    total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
+    _, stats, psnr0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                     stream=stream)
+    base_stats = stats[0].contiguous()
+    prev_dev = psnr0.clone()
+    init = float(psnr0.item())
+    prev = init
+    psnr_buf = torch.empty(k_max, dtype=torch.float64, device=dev)
+    gst_buf = torch.empty((k_max, 3), dtype=torch.float64, device=dev)
+    kdev = torch.empty(1, dtype=torch.int32, device=dev)
+    ctl = KController(k_min=k_min, k_max=k_max, k0=min(16, k_max))
+    pos, launches = 0, 0
+    acc_pos, acc_psnr = [], []
+    stopped = False
+    while pos < total:
+        k = min(ctl.k, total - pos)
+        flips = order_t[pos:pos + k]
+        plan.eval_flips(mask, target, base_stats, flips, psnr_buf[:k], gst_buf[:k], stream=stream)
+        launches += 1
+        ps = psnr_buf[:k].cpu().numpy()
+        i = first_improving(ps, prev)
+        ctl.update(i)
+        if i is None:
+            pos += k
+            continue
+        kdev.fill_(i)
+        plan.commit_flip(mask, base_stats, prev_dev, flips, psnr_buf, gst_buf, kdev, stream=stream)
+        prev = float(ps[i])
+        acc_pos.append(pos + i)
+        acc_psnr.append(prev)
+        pos += i + 1
+        if stop_diff is not None and prev - init >= stop_diff:      # DBS_ratio_0.5.py:366-372
+            stopped = True
+            break
+    return GreedyResult(init, prev, pos, acc_pos, acc_psnr, launches, stopped)
+
+
+@dataclass
+class ProbeResult:
+    base_psnr: float
+    psnr: np.ndarray                 # per flip
+    improved: np.ndarray             # psnr > base (strict)
+    attempted_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.int64))
+    improved_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.int64))
+    delta_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.float64))
+
+
+def premodel_bins(values: np.ndarray) -> np.ndarray:
+    """[0,.1),...,[.8,.9),[.9,1.0] -> 0..9; outside -> -1 (DBS_1024_24.py:289-300)."""
+    v = np.asarray(values, np.float64)
+    b = np.full(v.shape, -1, np.int64)
+    for i in range(10):
+        lo, hi = OUTPUT_BINS[i], OUTPUT_BINS[i + 1]
+        sel = (v >= lo) & ((v <= hi) if i == 9 else (v < hi))
+        b[sel & (b < 0)] = i
+    return b
+
+
+def probe(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips, pre_model: Optional[np.ndarray] = None,
+          stream=None) -> ProbeResult:
+    dev = plan.device
+    flips_t = torch.as_tensor(np.asarray(flips, np.int64)).to(dev)
+    _, stats, psnr0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                     stream=stream)
+    base = float(psnr0.item())
+    out = torch.empty(flips_t.shape[0], dtype=torch.float64, device=dev)
+    gst = torch.empty((flips_t.shape[0], 3), dtype=torch.float64, device=dev)
+    plan.eval_flips(mask, target, stats[0].contiguous(), flips_t, out, gst, stream=stream)
+    ps = out.cpu().numpy()
+    improved = ps > base
+    res = ProbeResult(base, ps, improved)
+    if pre_model is not None:
+        c = plan.cfg
+        f = np.asarray(flips, np.int64)
+        ch, k = f // (c.height * c.width), f % (c.height * c.width)
+        vals = np.asarray(pre_model)[ch, k // c.width, k % c.width]
+        bins = premodel_bins(vals)
+        for i in range(10):
+            sel = bins == i
+            res.attempted_bins[i] = int(sel.sum())
+            res.improved_bins[i] = int((sel & improved).sum())
+            res.delta_bins[i] = float(np.sum((ps - base)[sel & improved]))
+    return res

@@ -1,0 +1,314 @@
+"""Batched, device-resident binary-hologram environments.
+
+``HologramVecEnv`` is B copies of the reference's ``BinaryHologramEnv``
+(env.py:37-259; RGB per-flip intent of DBS_1024_24.py:313-422) stepped with
+one batched launch sequence: decode -> flip -> re-propagate the touched colour
+group -> relative PSNR -> reward / rollback / termination, all on the GPU
+(include/hbx.h hbx_env_step).  Observations stay on the device as torch
+tensors unless numpy is asked for.
+
+``BinaryHologramEnv`` is the drop-in single-env class with the reference
+constructor (target_function, trainloader, max_steps, T_PSNR, T_steps,
+T_PSNR_DIFF) and the gymnasium reset/step contract, backed by a B=1
+``HologramVecEnv``.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Iterable, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import spaces
+from .plan import OpticsConfig, Plan, mono_config, pack_bits, rgb_config, unpack_bits
+
+RW = 800.0   # env.py:29
+
+OBS_KEYS = ("state_record", "state", "pre_model", "recon_image", "target_image")
+
+
+class EnvState:
+    """Device buffers of B environments (env.py:65-81 attributes)."""
+
+    def __init__(self, plan: Plan, n_env: int, keep_record: bool = True, keep_pre_model: bool = True,
+                 keep_intensity: bool = True):
+        c, dev = plan.cfg, plan.device
+        self.plan, self.n = plan, n_env
+        self.mask = torch.zeros(plan.mask_shape(n_env), dtype=torch.int64, device=dev)
+        self.record = torch.zeros((n_env, c.channels, c.height, c.width), dtype=torch.int8,
+                                  device=dev) if keep_record else None
+        self.target = torch.zeros(plan.target_shape(n_env), dtype=torch.float32, device=dev)
+        self.pre_model = torch.zeros((n_env, c.channels, c.height, c.width), dtype=torch.float32,
+                                     device=dev) if keep_pre_model else None
+        self.intensity = torch.zeros(plan.target_shape(n_env), dtype=torch.float32,
+                                     device=dev) if keep_intensity else None
+        self.chan_stats = torch.zeros((n_env, c.groups, 3), dtype=torch.float64, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.init_psnr = torch.zeros(n_env, **f64)
+        self.prev_psnr = torch.zeros(n_env, **f64)
+        self.max_psnr_diff = torch.full((n_env,), float("-inf"), **f64)
+        self.steps = torch.zeros(n_env, **i64)
+        self.flip_count = torch.zeros(n_env, **i64)
+        self.sustained = torch.zeros(n_env, **i64)
+        self.error = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.bufs = _lib.EnvBuffers()
+        p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        b = self.bufs
+        b.mask, b.record, b.target = p(self.mask), p(self.record), p(self.target)
+        b.chan_stats, b.init_psnr, b.prev_psnr = p(self.chan_stats), p(self.init_psnr), p(self.prev_psnr)
+        b.max_psnr_diff, b.steps, b.flip_count = p(self.max_psnr_diff), p(self.steps), p(self.flip_count)
+        b.sustained, b.intensity, b.error = p(self.sustained), p(self.intensity), p(self.error)
+
+    def check_error(self):
+        if int(self.error.item()) != 0:
+            self.error.zero_()
+            raise ValueError("action out of range [0, CH*H*W) passed to step()")
+
+
+class HologramVecEnv:
+    """B environments on one GPU, stepped together (SB3 VecEnv-style API).
+
+    target_source(i) -> target tensor [G, H, W] (or [1, G, H, W]) in [0, 1]
+    pre_model_fn(target[1, G, H, W]) -> pre-model output [1, CH, H, W] in [0, 1]
+    (env.py:106-120: the binary state is pre_model >= 0.5), or
+    pre_model_source(i) -> the same for env i directly (injected / synthetic).
+    """
+
+    def __init__(self, cfg: OpticsConfig, num_envs: int, target_source: Callable,
+                 pre_model_fn: Optional[Callable] = None, max_steps: int = 10000, T_PSNR: float = 30.0,
+                 T_steps: int = 1, T_PSNR_DIFF: float = 0.1, reward_weight: float = RW,
+                 accept_rule: int = _lib.ACCEPT_ENV, max_jobs: Optional[int] = None,
+                 obs_keys: Sequence[str] = OBS_KEYS, auto_reset: bool = True,
+                 device: Optional[int] = None, pre_model_source: Optional[Callable] = None):
+        if (pre_model_fn is None) == (pre_model_source is None):
+            raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
+        self.cfg = cfg
+        self.num_envs = int(num_envs)
+        self.plan = Plan(cfg, max_jobs=max_jobs or max(self.num_envs, cfg.groups), device=device)
+        self.device = self.plan.device
+        self.obs_keys = tuple(obs_keys)
+        for k in self.obs_keys:
+            if k not in OBS_KEYS:
+                raise ValueError(f"unknown obs key {k}")
+        self.state = EnvState(self.plan, self.num_envs,
+                              keep_record=True,
+                              keep_pre_model="pre_model" in self.obs_keys,
+                              keep_intensity="recon_image" in self.obs_keys)
+        self.target_source = target_source
+        self.pre_model_fn = pre_model_fn
+        self.pre_model_source = pre_model_source
+        self.auto_reset = auto_reset
+        self.params = _lib.EnvParams()
+        self.params.max_steps, self.params.t_psnr = int(max_steps), float(T_PSNR)
+        self.params.t_steps, self.params.t_psnr_diff = int(T_steps), float(T_PSNR_DIFF)
+        self.params.reward_weight, self.params.accept_rule = float(reward_weight), int(accept_rule)
+        c = cfg
+        self.num_pixels = c.channels * c.height * c.width
+        self.action_space = spaces.Discrete(self.num_pixels)           # env.py:50-52
+        self.observation_space = spaces.Dict({                          # env.py:42-48
+            "state_record": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
+            "state": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
+            "pre_model": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.float32),
+            "recon_image": spaces.Box(0, 1, (1, c.groups, c.height, c.width), np.float32),
+            "target_image": spaces.Box(0, 1, (1, c.groups, c.height, c.width), np.float32),
+        })
+        n, dev = self.num_envs, self.device
+        self._reward = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._psnr = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._acc = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self._term = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self._trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self._ginten = torch.zeros((n, c.height, c.width), dtype=torch.float32, device=dev) \
+            if "recon_image" in self.obs_keys else None
+        self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
+        self._actions = None
+        self.episode_count = 0
+
+    # -- reset -------------------------------------------------------------------
+    def _load_env(self, i: int):
+        c = self.cfg
+        tgt = self.target_source(i)
+        tgt = torch.as_tensor(tgt).to(self.device, torch.float32).reshape(1, c.groups, c.height, c.width)
+        with torch.no_grad():
+            pre = self.pre_model_fn(tgt) if self.pre_model_fn is not None else self.pre_model_source(i)
+        pre = torch.as_tensor(pre).to(self.device, torch.float32).reshape(c.channels, c.height, c.width)
+        st = self.state
+        st.target[i].copy_(tgt[0])
+        st.mask[i].copy_(pack_bits(pre >= 0.5))                       # env.py:120
+        if st.pre_model is not None:
+            st.pre_model[i].copy_(pre)
+        self.episode_count += 1
+
+    def reset_envs(self, env_ids: Sequence[int]):
+        ids = [int(i) for i in env_ids]
+        if not ids:
+            return
+        for i in ids:
+            self._load_env(i)
+        idt = torch.tensor(ids, dtype=torch.int32, device=self.device)
+        self.plan.env_reset(self.state.bufs, self.num_envs, idt)      # env.py:121-133
+
+    def reset(self, seed=None, options=None):
+        self.reset_envs(range(self.num_envs))
+        if self._ginten is not None and self.state.intensity is not None:
+            self._ginten.zero_()
+        return self.observe(stepped=False)
+
+    # -- step --------------------------------------------------------------------
+    def step_async(self, actions):
+        self._actions = actions
+
+    def step_wait(self):
+        return self.step(self._actions)
+
+    def step_device(self, actions: torch.Tensor):
+        """One batched env.step (no host sync): returns device tensors
+        (reward f64, psnr f64, accepted u8, terminated u8, truncated u8)."""
+        if not isinstance(actions, torch.Tensor) or actions.device != self.device \
+                or actions.dtype != torch.int64:
+            actions = torch.as_tensor(np.asarray(actions, np.int64) if not isinstance(actions, torch.Tensor)
+                                      else actions).to(self.device, torch.int64)
+        actions = actions.reshape(self.num_envs).contiguous()
+        self._last_actions = actions
+        self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, self._reward, self._psnr,
+                           self._acc, self._term, self._trunc, self._ginten)
+        return self._reward, self._psnr, self._acc, self._term, self._trunc
+
+    def step(self, actions):
+        """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset."""
+        reward, psnr, acc, term, trunc = self.step_device(actions)
+        self.state.check_error()
+        obs = self.observe(stepped=True)
+        r = reward.cpu().numpy()
+        t = term.cpu().numpy().astype(bool)
+        tr = trunc.cpu().numpy().astype(bool)
+        dones = t | tr
+        infos = [{} for _ in range(self.num_envs)]
+        if self.auto_reset and dones.any():
+            done_ids = np.nonzero(dones)[0].tolist()
+            term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}
+            for j, i in enumerate(done_ids):
+                infos[i]["terminal_observation"] = {k: v[j] for k, v in term_obs.items()}
+                infos[i]["TimeLimit.truncated"] = bool(tr[i] and not t[i])
+            self.reset_envs(done_ids)
+            obs = self.observe(stepped=False)
+        return obs, r, dones, infos
+
+    # -- observations (env.py:135-140,176-181) ----------------------------------------
+    def observe(self, stepped: bool):
+        st, c = self.state, self.cfg
+        out = {}
+        for k in self.obs_keys:
+            if k == "state_record":
+                out[k] = st.record.unsqueeze(1)
+            elif k == "state":
+                out[k] = unpack_bits(st.mask, c.width).unsqueeze(1)
+            elif k == "pre_model":
+                out[k] = st.pre_model.unsqueeze(1)
+            elif k == "target_image":
+                out[k] = st.target.unsqueeze(1)
+            elif k == "recon_image":
+                rec = st.intensity.clone()
+                if stepped and self._ginten is not None:
+                    # the reference returns the stepped (pre-rollback) recon (env.py:179)
+                    g = (self._last_actions // (c.height * c.width)) // c.planes
+                    rec[torch.arange(self.num_envs, device=self.device), g] = self._ginten
+                out[k] = rec.unsqueeze(1)
+        return out
+
+    # -- gym-ish accessors ------------------------------------------------------------
+    @property
+    def initial_psnr(self):
+        return self.state.init_psnr
+
+    @property
+    def previous_psnr(self):
+        return self.state.prev_psnr
+
+    def close(self):
+        self.plan.close()
+
+
+def _to_numpy(obs: dict):
+    return {k: v.detach().cpu().numpy() for k, v in obs.items()}
+
+
+class BinaryHologramEnv(spaces.EnvBase):
+    """Drop-in for the reference ``BinaryHologramEnv`` (env.py:37-259).
+
+    target_function: pre-model (env.py:110); trainloader yields (target, path)
+    (env.py:96-102).  ``config`` selects the optics: mono 256x256x8 (env.py)
+    by default; pass ``rgb_config(1024)`` for env_1024_24.py.  Observations
+    are numpy dicts like the reference; scalars are Python floats."""
+
+    def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 device: Optional[int] = None):
+        super().__init__()
+        self.cfg = config or mono_config(256)
+        self.target_function = target_function
+        self.trainloader = trainloader
+        self.data_iter = iter(self.trainloader)
+        self.max_steps, self.T_PSNR, self.T_steps, self.T_PSNR_DIFF = max_steps, T_PSNR, T_steps, T_PSNR_DIFF
+        self.verbose = verbose
+        self.current_file = None
+        self._vec = HologramVecEnv(self.cfg, 1, self._next_target, self._pre_model, max_steps=max_steps,
+                                   T_PSNR=T_PSNR, T_steps=T_steps, T_PSNR_DIFF=T_PSNR_DIFF,
+                                   auto_reset=False, device=device)
+        self.observation_space = self._vec.observation_space
+        self.action_space = self._vec.action_space
+        self.num_pixels = self._vec.num_pixels
+        self.episode_num_count = 0
+        self.initial_psnr = None
+        self.previous_psnr = None
+        self.steps = 0
+        self.flip_count = 0
+        self.psnr_sustained_steps = 0
+
+    def _next_target(self, i):
+        try:                                                           # env.py:96-102
+            target, self.current_file = next(self.data_iter)
+        except StopIteration:
+            if self.verbose:
+                print("\033[40;93m[INFO] Reached the end of dataset. Restarting from the beginning.\033[0m")
+            self.data_iter = iter(self.trainloader)
+            target, self.current_file = next(self.data_iter)
+        return target
+
+    def _pre_model(self, target):
+        out = self.target_function(target)
+        self.observation = out
+        return out
+
+    @property
+    def state(self):
+        return unpack_bits(self._vec.state.mask[0], self.cfg.width).unsqueeze(0).cpu().numpy()
+
+    def reset(self, seed=None, options=None):
+        self.episode_num_count += 1
+        obs = _to_numpy(self._vec.reset())
+        self.initial_psnr = float(self._vec.state.init_psnr[0].item())
+        self.previous_psnr = self.initial_psnr
+        self.steps = self.flip_count = self.psnr_sustained_steps = 0
+        self.total_start_time = time.time()
+        if self.verbose:
+            print(f"\033[92mInitial PSNR: {self.initial_psnr:.6f}\033[0m")
+        return obs, {"state": obs.get("state")}
+
+    def step(self, action):
+        a = torch.tensor([int(action)], dtype=torch.int64, device=self._vec.device)
+        reward, psnr, acc, term, trunc = self._vec.step_device(a)
+        self._vec.state.check_error()
+        obs = _to_numpy(self._vec.observe(stepped=True))
+        st = self._vec.state
+        self.steps = int(st.steps[0].item())
+        self.flip_count = int(st.flip_count[0].item())
+        self.psnr_sustained_steps = int(st.sustained[0].item())
+        self.previous_psnr = float(st.prev_psnr[0].item())
+        return obs, float(reward[0].item()), bool(term[0].item()), bool(trunc[0].item()), {}
+
+    def close(self):
+        self._vec.close()

@@ -1,0 +1,242 @@
+"""Plan: one propagation configuration on one GPU (wraps hbx_plan_t).
+
+Mirrors what ``tt.simulate(tt.Tensor(x, meta={'dx','wl'}), z)`` +
+``tt.relativeLoss(.., tm.get_PSNR)`` compute in the reference
+(env.py:123-133,170-174; DBS_1024_24.py:244-257,326-332), but for a whole
+batch of bit-packed masks at once, entirely on the device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+
+PIXEL_PITCH = 7.56e-6          # env.py:124
+Z_DEFAULT = 2e-3               # env.py:90
+WL_MONO = (515e-9,)            # env.py:124
+WL_RGB = (638e-9, 515e-9, 450e-9)   # env_1024_24.py:135-138
+
+
+@dataclass
+class OpticsConfig:
+    height: int
+    width: int
+    groups: int = 1
+    planes: int = 8
+    wavelengths: Sequence[float] = WL_MONO
+    dx: float = PIXEL_PITCH
+    dy: float = PIXEL_PITCH
+    z: float = Z_DEFAULT
+    tf_kind: int = _lib.TF_ASM
+    field_kind: int = _lib.FIELD_AMPLITUDE
+    rel_scale: int = _lib.REL_LSQ
+    peak: float = 1.0
+
+    @property
+    def channels(self) -> int:
+        return self.groups * self.planes
+
+    @property
+    def words(self) -> int:
+        return self.width // 64
+
+    def to_c(self) -> _lib.Optics:
+        o = _lib.Optics()
+        o.height, o.width, o.groups, o.planes = self.height, self.width, self.groups, self.planes
+        wl = list(self.wavelengths)
+        if len(wl) != self.groups:
+            raise ValueError(f"{len(wl)} wavelengths for {self.groups} groups")
+        for i, w in enumerate(wl):
+            o.wavelength[i] = float(w)
+        o.dx, o.dy, o.z = float(self.dx), float(self.dy), float(self.z)
+        o.tf_kind, o.field_kind, o.rel_scale = int(self.tf_kind), int(self.field_kind), int(self.rel_scale)
+        o.peak = float(self.peak)
+        return o
+
+
+def mono_config(n: int = 256, **kw) -> OpticsConfig:
+    """env.py: 1 group x 8 planes at 515 nm (IPS=256, CH=8)."""
+    return OpticsConfig(n, n, 1, 8, WL_MONO, **kw)
+
+
+def rgb_config(n: int = 1024, planes: int = 8, **kw) -> OpticsConfig:
+    """env_1024_24.py: 3 groups x 8 planes at 638/515/450 nm (IPS=1024, CH=24)."""
+    return OpticsConfig(n, n, 3, planes, WL_RGB, **kw)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(stream: Optional[torch.cuda.Stream]):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _need(t: torch.Tensor, name: str, dtype: torch.dtype, shape, device: torch.device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype} != {dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+    if t.device != device:
+        raise ValueError(f"{name}: device {t.device} != {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def pack_bits(mask: torch.Tensor) -> torch.Tensor:
+    """{0,1} tensor [..., H, W] -> int64 words [..., H, W/64] (bit j of word w = col 64w+j).
+
+    Runs on the tensor's device (torch ops; layout of include/hbx.h)."""
+    w = mask.shape[-1]
+    if w % 64:
+        raise ValueError("width must be a multiple of 64")
+    m = (mask != 0).to(torch.int64).reshape(*mask.shape[:-1], w // 64, 64)
+    shifts = torch.arange(64, device=mask.device, dtype=torch.int64)
+    return (m << shifts).sum(dim=-1, dtype=torch.int64)   # bit 63 wraps into the sign: same bits
+
+
+def unpack_bits(words: torch.Tensor, width: int) -> torch.Tensor:
+    shifts = torch.arange(64, device=words.device, dtype=torch.int64)
+    bits = (words.unsqueeze(-1) >> shifts) & 1
+    return bits.reshape(*words.shape[:-1], width).to(torch.int8)
+
+
+class Plan:
+    """hbx_plan_t owner.  ``max_jobs`` bounds the group propagations in flight
+    (workspace = max_jobs * planes * N^2 * 8 bytes)."""
+
+    def __init__(self, cfg: OpticsConfig, max_jobs: int = 8, device: Optional[int] = None):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("hbx.Plan needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.cfg = cfg
+        self.device_index = torch.cuda.current_device() if device is None else int(device)
+        self.device = torch.device("cuda", self.device_index)
+        self.max_jobs = int(max_jobs)
+        h = C.c_void_p()
+        oc = cfg.to_c()
+        with torch.cuda.device(self.device_index):
+            _lib.check(self.lib.hbx_plan_create(C.byref(h), C.byref(oc), self.max_jobs,
+                                                self.device_index), "hbx_plan_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.hbx_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def workspace_bytes(self) -> int:
+        return int(self.lib.hbx_plan_workspace_bytes(self._h))
+
+    # -- device timing of the three passes (hbx_plan_set_timing) --------------------
+    def set_timing(self, capacity: int):
+        _lib.check(self.lib.hbx_plan_set_timing(self._h, int(capacity)), "hbx_plan_set_timing")
+
+    def read_timing(self):
+        """{pass: (total_ms, launches, jobs)} for k_rowfwd / k_col / k_rowinv (syncs)."""
+        ms = (C.c_double * _lib.NUM_PASSES)()
+        n = (C.c_int64 * _lib.NUM_PASSES)()
+        jobs = (C.c_int64 * _lib.NUM_PASSES)()
+        _lib.check(self.lib.hbx_plan_read_timing(self._h, ms, n, jobs), "hbx_plan_read_timing")
+        return {name: (ms[i], n[i], jobs[i]) for i, name in enumerate(_lib.PASS_NAMES)}
+
+    # -- buffer helpers -------------------------------------------------------
+    def mask_shape(self, n_env: int):
+        c = self.cfg
+        return (n_env, c.channels, c.height, c.words)
+
+    def target_shape(self, n_env: int):
+        c = self.cfg
+        return (n_env, c.groups, c.height, c.width)
+
+    def _check_mask_target(self, mask, target, n):
+        _need(mask, "mask", torch.int64, self.mask_shape(n), self.device)
+        _need(target, "target", torch.float32, self.target_shape(n), self.device)
+
+    # -- operators ---------------------------------------------------------------
+    def propagate(self, mask: torch.Tensor, target: torch.Tensor, want_intensity: bool = True,
+                  stream=None):
+        """Full propagation of every group: returns (intensity|None, chan_stats, psnr)."""
+        n = mask.shape[0]
+        self._check_mask_target(mask, target, n)
+        c = self.cfg
+        inten = torch.empty((n, c.groups, c.height, c.width), dtype=torch.float32,
+                            device=self.device) if want_intensity else None
+        stats = torch.empty((n, c.groups, 3), dtype=torch.float64, device=self.device)
+        psnr = torch.empty((n,), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_propagate(self._h, _ptr(mask), _ptr(target), n, _ptr(inten),
+                                          _ptr(stats), _ptr(psnr), _stream(stream)), "hbx_propagate")
+        return inten, stats, psnr
+
+    def psnr(self, chan_stats: torch.Tensor, stream=None) -> torch.Tensor:
+        n = chan_stats.shape[0]
+        _need(chan_stats, "chan_stats", torch.float64, (n, self.cfg.groups, 3), self.device)
+        out = torch.empty((n,), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_psnr(self._h, _ptr(chan_stats), n, _ptr(out), _stream(stream)), "hbx_psnr")
+        return out
+
+    def eval_flips(self, base_mask: torch.Tensor, target: torch.Tensor, base_stats: torch.Tensor,
+                   flips: torch.Tensor, psnr_out: Optional[torch.Tensor] = None,
+                   group_stats: Optional[torch.Tensor] = None, stream=None):
+        """PSNR of K independent single-pixel flips of ONE base env."""
+        c = self.cfg
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
+        k = flips.shape[0]
+        _need(flips, "flips", torch.int64, (k,), self.device)
+        if psnr_out is None:
+            psnr_out = torch.empty((k,), dtype=torch.float64, device=self.device)
+        if group_stats is None:
+            group_stats = torch.empty((k, 3), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_eval_flips(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                           _ptr(flips), k, _ptr(psnr_out), _ptr(group_stats),
+                                           _stream(stream)), "hbx_eval_flips")
+        return psnr_out, group_stats
+
+    def commit_flip(self, base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats,
+                    k_dev: torch.Tensor, stream=None):
+        _lib.check(self.lib.hbx_commit_flip(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),
+                                            _ptr(flips), _ptr(psnr_out), _ptr(group_stats), _ptr(k_dev),
+                                            _stream(stream)), "hbx_commit_flip")
+
+    def step(self, mask, actions, target, chan_stats, prev_psnr, accept_rule=_lib.ACCEPT_DBS,
+             stream=None):
+        """DBS primitive (include/hbx.h hbx_step): returns (psnr, accepted)."""
+        n = mask.shape[0]
+        self._check_mask_target(mask, target, n)
+        _need(actions, "actions", torch.int64, (n,), self.device)
+        psnr = torch.empty((n,), dtype=torch.float64, device=self.device)
+        acc = torch.empty((n,), dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.hbx_step(self._h, _ptr(mask), _ptr(actions), n, _ptr(target), _ptr(chan_stats),
+                                     _ptr(prev_psnr), _ptr(psnr), _ptr(acc), int(accept_rule),
+                                     _stream(stream)), "hbx_step")
+        return psnr, acc
+
+    # env-level entry points are used by hbx.env (EnvState owns the buffers)
+    def env_reset(self, bufs: _lib.EnvBuffers, n_env: int, env_ids: Optional[torch.Tensor] = None,
+                  stream=None):
+        n_ids = 0 if env_ids is None else int(env_ids.shape[0])
+        _lib.check(self.lib.hbx_env_reset(self._h, C.byref(bufs), n_env, _ptr(env_ids), n_ids,
+                                          _stream(stream)), "hbx_env_reset")
+
+    def env_step(self, bufs, params, n_env, actions, reward, psnr, accepted, terminated, truncated,
+                 group_intensity=None, stream=None):
+        _lib.check(self.lib.hbx_env_step(self._h, C.byref(bufs), C.byref(params), n_env, _ptr(actions),
+                                         _ptr(reward), _ptr(psnr), _ptr(accepted), _ptr(terminated),
+                                         _ptr(truncated), _ptr(group_intensity), _stream(stream)),
+                   "hbx_env_step")

@@ -1,0 +1,190 @@
+/*
+ * hbx.h -- C-ABI of the MI355X-native binary-hologram hot path (libhbx.so).
+ *
+ * The reference (songyb111-gachon/binary-hologram-reinforcement-learning) is
+ * pure Python: its hot path is a chain of torch ops behind the third-party
+ * `torchOptics` API (tt.Tensor / tt.simulate / tt.relativeLoss / tm.get_PSNR)
+ * called from gymnasium envs and DBS drivers.  This header is the boundary
+ * those call sites bind to once the hot path is native.  Each entry point
+ * names the reference interface it replaces (file:line under the reference).
+ *
+ * Conventions
+ *   - Every buffer argument is a caller-owned DEVICE pointer (e.g. a
+ *     torch-ROCm tensor's data_ptr()), contiguous, in the layout stated.
+ *   - Masks are bit-packed: uint64 words [..][H][W/64], bit j of word w is
+ *     pixel column 64*w + j (little-endian).  W % 64 == 0.
+ *   - All calls are asynchronous on `stream` (a hipStream_t; NULL = default).
+ *     A plan is bound to one device and is not re-entrant: one plan per
+ *     stream / per GPU process.
+ *   - Return 0 on success, a negative HBX_ERR_* code otherwise; the message
+ *     is in hbx_last_error() (thread-local).  No C++ exception crosses it.
+ *   - Channel c of an env belongs to colour group g = c / planes; group g
+ *     propagates with wavelength[g]  (env_1024_24.py:135-147).
+ */
+#ifndef HBX_H
+#define HBX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HBX_ABI_VERSION 1
+
+#define HBX_OK 0
+#define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
+#define HBX_ERR_HIP (-2)         /* HIP runtime error                             */
+#define HBX_ERR_UNSUPPORTED (-3) /* size not built (N must be 64, 256 or 1024)    */
+#define HBX_ERR_NOMEM (-4)       /* workspace allocation failed                   */
+
+/* Transfer function (tt.simulate, env.py:172; SURVEY a4 assumptions as switches) */
+#define HBX_TF_ASM 0       /* exact angular spectrum, evanescent cut              */
+#define HBX_TF_FRESNEL 1   /* Fresnel transfer function                           */
+/* Mask -> field (env.py:170-171) */
+#define HBX_FIELD_AMPLITUDE 0 /* u = m in {0,1}  (literal reference)              */
+#define HBX_FIELD_PHASE 1     /* u = exp(i pi m) in {+1,-1}                       */
+/* tt.relativeLoss scale (env.py:174) */
+#define HBX_REL_NONE 0
+#define HBX_REL_LSQ 1      /* s = sum(I T)/sum(I^2) over every channel            */
+/* accept rule */
+#define HBX_ACCEPT_ENV 0   /* roll back iff delta < 0   (env.py:191)              */
+#define HBX_ACCEPT_DBS 1   /* accept iff psnr > prev    (DBS_1024_24.py:355)      */
+
+#define HBX_MAX_GROUPS 4
+
+/* Optics of one plan; replaces tt.Tensor meta {'dx','wl'} + simulate's z
+ * (env.py:124,172; env_1024_24.py:135-138; DBS_1024_24.py:230-233). */
+typedef struct hbx_optics {
+  int32_t height;                        /* N (64, 256 or 1024), square      */
+  int32_t width;                         /* == height                         */
+  int32_t groups;                        /* G: 1 mono, 3 RGB                  */
+  int32_t planes;                        /* P planes per group (even)         */
+  double wavelength[HBX_MAX_GROUPS];     /* metres, per group                 */
+  double dx, dy;                         /* pixel pitch, metres               */
+  double z;                              /* propagation distance, metres      */
+  int32_t tf_kind;                       /* HBX_TF_*                          */
+  int32_t field_kind;                    /* HBX_FIELD_*                       */
+  int32_t rel_scale;                     /* HBX_REL_*                         */
+  int32_t reserved;
+  double peak;                           /* PSNR peak (1.0)                   */
+} hbx_optics_t;
+
+/* Device-resident state of B environments (BinaryHologramEnv attributes,
+ * env.py:65-81: state, state_record, previous/initial psnr, counters). */
+typedef struct hbx_env_buffers {
+  uint64_t* mask;          /* [B][G*P][H][W/64]  env.state                    */
+  int8_t* record;          /* [B][G*P][H][W]     env.state_record (nullable)  */
+  const float* target;     /* [B][G][H][W]       target image                 */
+  double* chan_stats;      /* [B][G][3]          sum I*T, sum I^2, sum T^2    */
+  double* init_psnr;       /* [B]                env.initial_psnr             */
+  double* prev_psnr;       /* [B]                env.previous_psnr            */
+  double* max_psnr_diff;   /* [B]                env.max_psnr_diff            */
+  int64_t* steps;          /* [B]                env.steps                    */
+  int64_t* flip_count;     /* [B]                env.flip_count               */
+  int64_t* sustained;      /* [B]                env.psnr_sustained_steps     */
+  float* intensity;        /* [B][G][H][W] cached group means (nullable)      */
+  int32_t* error;          /* [1] sticky device error word (nullable)         */
+} hbx_env_buffers_t;
+
+/* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
+typedef struct hbx_env_params {
+  int64_t max_steps;       /* 10000 */
+  double t_psnr;           /* 30    */
+  int64_t t_steps;         /* 1     */
+  double t_psnr_diff;      /* 0.1   */
+  double reward_weight;    /* 800   */
+  int32_t accept_rule;     /* HBX_ACCEPT_ENV */
+  int32_t reserved;
+} hbx_env_params_t;
+
+typedef struct hbx_plan* hbx_plan_t;
+
+/* Library identity. */
+int hbx_abi_version(void);
+const char* hbx_last_error(void);
+
+/* Plan: owns twiddles, transfer-function tables and a workspace for up to
+ * `max_jobs` concurrent group propagations (64 MiB per job at N=1024).
+ * Replaces the per-call setup hidden inside tt.simulate (env.py:172). */
+int hbx_plan_create(hbx_plan_t* plan, const hbx_optics_t* optics, int32_t max_jobs,
+                    int32_t device);
+int hbx_plan_destroy(hbx_plan_t plan);
+size_t hbx_plan_workspace_bytes(hbx_plan_t plan);
+
+/* Full propagation of every group of n_env masks (env.py:123-133 reset path,
+ * env_1024_24.py:149-166, DBS_1024_24.py:244-257):
+ *   intensity[B][G][H][W] = mean_p |IFFT2(FFT2(u_p) H_g)|^2   (nullable)
+ *   chan_stats[B][G][3]   = per-channel sum I*T, sum I^2, sum T^2
+ *   psnr[B]               = relativeLoss(rgb, target, get_PSNR)  (nullable)  */
+int hbx_propagate(hbx_plan_t plan, const uint64_t* mask, const float* target, int32_t n_env,
+                  float* intensity, double* chan_stats, double* psnr, void* stream);
+
+/* PSNR from per-channel statistics (tt.relativeLoss(.., tm.get_PSNR),
+ * env.py:174): chan_stats[B][G][3] -> psnr[B]. */
+int hbx_psnr(hbx_plan_t plan, const double* chan_stats, int32_t n_env, double* psnr,
+             void* stream);
+
+/* Env reset tail (env.py:120-133): given env.mask already thresholded and
+ * env.target set for the listed envs (env_ids nullable = all n_env), propagate
+ * every group, fill chan_stats / intensity, set init_psnr = prev_psnr and zero
+ * steps / flip_count / sustained / record, max_psnr_diff = -inf. */
+int hbx_env_reset(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
+                  const int32_t* env_ids, int32_t n_ids, void* stream);
+
+/* Batched env.step(action) (env.py:154-259 mono; DBS_1024_24.py:313-422
+ * per-flip RGB with cached other-group statistics).  One action per env:
+ * decode (env.py:157-161), flip + record, re-propagate the touched colour
+ * group, relative PSNR, reward = RW * delta, rollback / bonus / termination.
+ *   reward, psnr [B] f64; accepted, terminated, truncated [B] u8 (nullable)
+ *   group_intensity [B][H][W] f32: the stepped (pre-rollback) group mean, the
+ *   obs "recon_image" channel (nullable).  Accepted steps also refresh
+ *   env->intensity[b][g] when that cache is non-null. */
+int hbx_env_step(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_env_params_t* params,
+                 int32_t n_env, const int64_t* actions, double* reward, double* psnr,
+                 uint8_t* accepted, uint8_t* terminated, uint8_t* truncated,
+                 float* group_intensity, void* stream);
+
+/* DBS primitive (SURVEY 8b hbx_step): one candidate flip per env evaluated
+ * against prev_psnr and applied iff accepted (accept_rule), without the
+ * env's reward bookkeeping (DBS.py:247-294). */
+int hbx_step(hbx_plan_t plan, uint64_t* mask, const int64_t* actions, int32_t n_env,
+             const float* target, double* chan_stats, double* prev_psnr, double* psnr_out,
+             uint8_t* accepted, int32_t accept_rule, void* stream);
+
+/* Independent trial flips against ONE fixed base env (probe sweep
+ * DBS_1024_24-128.py:310-373, range.py:294-335, env_group.py:96-120 and the
+ * speculative batches of greedy DBS): for k < K
+ *   psnr_out[k]      = PSNR with pixel flips[k] toggled
+ *   group_stats[k][3] = stats of the touched group (nullable)            */
+int hbx_eval_flips(hbx_plan_t plan, const uint64_t* base_mask, const float* target,
+                   const double* base_chan_stats, const int64_t* flips, int32_t K,
+                   double* psnr_out, double* group_stats, void* stream);
+
+/* Commit one accepted candidate of hbx_eval_flips into the base env:
+ * toggle mask bit `flips[k]`, chan_stats[g] = group_stats[k], prev_psnr =
+ * psnr_out[k].  Device-side; `k` is a device int32 (from the host or a
+ * device search). */
+int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stats,
+                    double* prev_psnr, const int64_t* flips, const double* psnr_out,
+                    const double* group_stats, const int32_t* k, void* stream);
+
+/* Optional device timing of the three propagation passes (hipEvents recorded
+ * on the launch stream around every pass launch; not for graph capture).
+ * capacity = max launches recorded per pass before hbx_plan_read_timing;
+ * 0 disables.  Replaces debug_env.py:165-306's per-phase time.time() prints. */
+#define HBX_PASS_ROWFWD 0
+#define HBX_PASS_COL 1
+#define HBX_PASS_ROWINV 2
+#define HBX_NUM_PASSES 3
+int hbx_plan_set_timing(hbx_plan_t plan, int32_t capacity);
+/* Waits for the recorded events; ms_total[HBX_NUM_PASSES] = summed kernel
+ * time, launches[HBX_NUM_PASSES], jobs[HBX_NUM_PASSES] = summed jobs per
+ * launch; then clears the record. */
+int hbx_plan_read_timing(hbx_plan_t plan, double* ms_total, int64_t* launches, int64_t* jobs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HBX_H */

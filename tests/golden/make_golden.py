@@ -1,0 +1,133 @@
+"""Generate the committed golden fixtures from the oracle (oracle/hbx_oracle.py).
+
+The reference cannot run here (torchOptics / gymnasium / SB3 / torchvision
+absent), so these vectors are the oracle's own float64 outputs on
+seeded inputs, plus the reference's stated known answers (env.py:228-229).
+They pin (a) the oracle against silent drift and (b) the HIP path in the
+-m gpu parity tests.  Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import hbx_oracle as O  # noqa: E402
+
+COMBOS = [(tf, fk, rs) for tf in (O.TF_ASM, O.TF_FRESNEL)
+          for fk in (O.FIELD_AMPLITUDE, O.FIELD_PHASE) for rs in (O.REL_LSQ, O.REL_NONE)]
+
+
+def small_rgb_cfg(**kw):
+    # 64x64, 3 colour groups x 2 planes: the smallest shape exercising every
+    # code path of the RGB env (group selection, cached other-group stats)
+    return O.OpticsConfig(64, 64, 3, 2, O.WL_RGB, **kw)
+
+
+def decode_table():
+    rows = []
+    rng = np.random.default_rng(7)
+    for (n, ch) in ((256, 8), (1024, 24)):
+        hw = n * n
+        edges = [0, hw - 1, hw, ch * hw - 1, n - 1, n, 5 * hw + 3 * n + 7]
+        rand = rng.integers(0, ch * hw, 25).tolist()
+        for a in edges + rand:
+            c, r, col = O.decode_action(a, n, n)
+            rows.append((n, ch, a, int(c), int(r), int(col)))
+    return np.array(rows, np.int64)
+
+
+def reward_table():
+    s = np.array([1.0, 0.5, 0.25, 0.125, 0.0, 0.3333333333333333])
+    return s, np.array([O.success_cubic(v) for v in s]), np.array([O.max_steps_cubic(v) for v in s])
+
+
+def prop_fixture(cfg_fn, seed):
+    cfg = cfg_fn()
+    pre, tgt = O.synthetic_inputs(cfg, seed)
+    mask = (pre >= 0.5).astype(np.uint8)
+    out = {"mask_bits": O.pack_mask(mask), "target": tgt, "seed": np.int64(seed),
+           "combos": np.array(COMBOS, np.int64)}
+    stats_all, psnr_all = [], []
+    for (tf, fk, rs) in COMBOS:
+        c = cfg_fn(tf_kind=tf, field_kind=fk, rel_scale=rs)
+        prop = O.Propagator(c)
+        inten = prop.all_intensity(mask)
+        st = np.stack([O.chan_stats(inten[g], tgt[g]) for g in range(c.groups)])
+        stats_all.append(st)
+        psnr_all.append(prop.psnr(st))
+        if (tf, fk, rs) == COMBOS[0]:
+            out["intensity"] = inten.astype(np.float32)
+            out["psnr_direct"] = np.float64(O.relative_psnr(inten, tgt, rs))
+    out["stats"] = np.array(stats_all)
+    out["psnr"] = np.array(psnr_all)
+    return out
+
+
+def env_trace(steps=200):
+    cfg = small_rgb_cfg()
+    pre, tgt = O.synthetic_inputs(cfg, 11)
+    env = O.OracleEnv(cfg, max_steps=150, T_PSNR=30.0, T_steps=1, T_PSNR_DIFF=0.08)
+    env.reset(pre, tgt)
+    acts = np.random.default_rng(12).integers(0, cfg.channels * 64 * 64, steps)
+    rec = [env.step(int(a)) for a in acts]
+    return {"pre_model": pre, "target": tgt, "actions": acts.astype(np.int64),
+            "initial_psnr": np.float64(env.initial_psnr),
+            "psnr": np.array([r.psnr for r in rec]), "reward": np.array([r.reward for r in rec]),
+            "accepted": np.array([r.accepted for r in rec]),
+            "terminated": np.array([r.terminated for r in rec]),
+            "truncated": np.array([r.truncated for r in rec]),
+            "final_mask_bits": O.pack_mask(env.state.astype(np.uint8)),
+            "final_record": env.state_record.copy(),
+            "params": np.array([150, 30.0, 1, 0.08])}
+
+
+def dbs_trace(n=4096):
+    cfg = small_rgb_cfg()
+    pre, tgt = O.synthetic_inputs(cfg, 21)
+    env = O.OracleEnv(cfg, accept_rule=1)
+    env.reset(pre, tgt)
+    order = np.random.default_rng(3).permutation(cfg.channels * 64 * 64)[:n].astype(np.int64)
+    acc, psnrs, final = O.dbs_greedy(env, order)
+    return {"pre_model": pre, "target": tgt, "order": order, "accepted": acc, "psnr": psnrs,
+            "initial_psnr": np.float64(env.initial_psnr), "final_psnr": np.float64(final),
+            "final_mask_bits": O.pack_mask(env.state.astype(np.uint8))}
+
+
+def probe_fixture(n=2048):
+    cfg = small_rgb_cfg()
+    pre, tgt = O.synthetic_inputs(cfg, 31)
+    env = O.OracleEnv(cfg)
+    base = env.reset(pre, tgt)
+    flips = np.random.default_rng(32).integers(0, cfg.channels * 64 * 64, n).astype(np.int64)
+    ps = O.probe_sweep(env, flips)
+    improved = ps > base
+    att, imp, dsum = O.premodel_histogram(pre, flips, improved, ps - base, 64, 64)
+    return {"pre_model": pre, "target": tgt, "flips": flips, "psnr": ps, "base_psnr": np.float64(base),
+            "attempted": att, "improved": imp, "delta_sum": dsum}
+
+
+def build_all():
+    dt = decode_table()
+    s, succ, maxs = reward_table()
+    return {
+        "decode.npz": {"table": dt},
+        "reward.npz": {"success_ratio": s, "success_cubic": succ, "max_steps_cubic": maxs},
+        "prop_64_rgb.npz": prop_fixture(small_rgb_cfg, 101),
+        "prop_256_mono.npz": prop_fixture(lambda **kw: O.mono_config(256, **kw), 202),
+        "env_trace_64.npz": env_trace(),
+        "dbs_trace_64.npz": dbs_trace(),
+        "probe_64.npz": probe_fixture(),
+    }
+
+
+def main():
+    for name, arrays in build_all().items():
+        np.savez_compressed(os.path.join(HERE, name), **arrays)
+        print("wrote", name)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,82 @@
+"""C-ABI checks without a GPU: libhbx.so loads, exports every function
+include/hbx.h declares, and the ctypes mirrors match the C struct layouts."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "hbx.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hbx_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    fns = header_functions()
+    from hbx import _lib
+    assert set(fns) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_loads_and_exports_all_symbols():
+    from hbx import _lib
+    lib = _lib.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert lib.hbx_abi_version() == _lib.ABI_VERSION
+
+
+def test_nm_exports_are_c_linkage():
+    from hbx import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    syms = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    for name in header_functions():
+        assert name in syms, f"{name} not exported with C linkage"
+
+
+def _c_sizeof(struct_name):
+    """Compile a tiny C program against include/hbx.h and print sizeof/offsets."""
+    prog = f"""
+#include <stdio.h>
+#include <stddef.h>
+#include "hbx.h"
+int main(void) {{ printf("%zu\\n", sizeof({struct_name})); return 0; }}
+"""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        exe = os.path.join(d, "s")
+        open(c, "w").write(prog)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+
+
+@pytest.mark.parametrize("cname,pyname", [("hbx_optics_t", "Optics"), ("hbx_env_buffers_t", "EnvBuffers"),
+                                          ("hbx_env_params_t", "EnvParams")])
+def test_struct_layout_matches(cname, pyname):
+    from hbx import _lib
+    assert C.sizeof(getattr(_lib, pyname)) == _c_sizeof(cname)
+
+
+def test_null_plan_is_an_error_not_a_crash():
+    from hbx import _lib
+    lib = _lib.load()
+    rc = lib.hbx_psnr(None, None, 0, None, None)
+    assert rc == _lib.ERR_INVALID
+    assert b"null plan" in lib.hbx_last_error()
+
+
+def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
+    import importlib
+    import hbx._lib as L
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(ImportError):
+        L.load()

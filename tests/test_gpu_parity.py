@@ -1,0 +1,271 @@
+"""Parity of the HIP path (libhbx.so via hbx) with the float64 oracle.
+
+Tolerances (north_star: "PSNR within 1e-4 of numpy"):
+  PSNR            |gpu - oracle| <= 1e-4 dB
+  channel stats   relative 2e-5 (fp32 FFT, f64 accumulation)
+  intensity       max |gpu - oracle| <= 2e-5 * max(oracle)
+  flip indexing, masks, records, accept / terminate / truncate flags: bit-exact
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import hbx_oracle as O  # noqa: E402
+
+PSNR_TOL = 1e-4
+STATS_RTOL = 2e-5
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+
+
+def dev_cfg(o: O.OpticsConfig):
+    import hbx
+    return hbx.OpticsConfig(o.height, o.width, o.groups, o.planes, tuple(o.wavelengths), o.dx, o.dy, o.z,
+                            o.tf_kind, o.field_kind, o.rel_scale, o.peak)
+
+
+def small_rgb(**kw):
+    return O.OpticsConfig(64, 64, 3, 2, O.WL_RGB, **kw)
+
+
+def load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def to_dev_bits(bits: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(bits).view(np.int64)).cuda()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    _require_gpu()
+    import hbx
+    hbx.load_library()
+    yield
+
+
+# -- propagation -------------------------------------------------------------------------
+@pytest.mark.parametrize("name,fn", [("prop_64_rgb.npz", small_rgb),
+                                     ("prop_256_mono.npz", lambda **kw: O.mono_config(256, **kw))])
+def test_propagate_golden_all_switches(golden_dir, name, fn):
+    import hbx
+    d = load(golden_dir, name)
+    bits = to_dev_bits(d["mask_bits"])[None]
+    tgt = torch.from_numpy(d["target"]).cuda()[None]
+    for i, (tf, fk, rs) in enumerate(d["combos"]):
+        cfg = dev_cfg(fn(tf_kind=int(tf), field_kind=int(fk), rel_scale=int(rs)))
+        plan = hbx.Plan(cfg, max_jobs=cfg.groups)
+        inten, stats, psnr = plan.propagate(bits, tgt)
+        torch.cuda.synchronize()
+        st = stats[0].cpu().numpy()
+        assert np.allclose(st, d["stats"][i], rtol=STATS_RTOL), (tf, fk, rs)
+        assert abs(float(psnr[0]) - float(d["psnr"][i])) <= PSNR_TOL, (tf, fk, rs)
+        if i == 0:
+            ref = d["intensity"]
+            got = inten[0].cpu().numpy()
+            assert np.max(np.abs(got - ref)) <= 2e-5 * np.max(ref)
+        plan.close()
+
+
+def test_propagate_1024_rgb_vs_oracle():
+    import hbx
+    ocfg = O.rgb_config(1024)
+    pre, tgt = O.synthetic_inputs(ocfg, 0)
+    mask = (pre >= 0.5).astype(np.uint8)
+    prop = O.Propagator(ocfg)
+    ref_i = prop.all_intensity(mask)
+    ref_st = np.stack([O.chan_stats(ref_i[g], tgt[g]) for g in range(3)])
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=3)
+    inten, stats, psnr = plan.propagate(to_dev_bits(O.pack_mask(mask))[None], torch.from_numpy(tgt).cuda()[None])
+    torch.cuda.synchronize()
+    assert np.allclose(stats[0].cpu().numpy(), ref_st, rtol=STATS_RTOL)
+    assert abs(float(psnr[0]) - prop.psnr(ref_st)) <= PSNR_TOL
+    got = inten[0].cpu().numpy()
+    assert np.max(np.abs(got - ref_i)) <= 2e-5 * np.max(ref_i)
+
+
+def test_parseval_full_size_batch():
+    """Size-independent property at the benchmark size (1024 x 24, B=4):
+    sum_xy I_g = popcount(group) / P exactly (|H| = 1, no evanescent cut)."""
+    import hbx
+    cfg = hbx.rgb_config(1024)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    pre = torch.rand((4, 24, 1024, 1024), generator=g, device="cuda")
+    bits = hbx.pack_bits(pre >= 0.5)
+    tgt = torch.rand((4, 3, 1024, 1024), generator=g, device="cuda")
+    plan = hbx.Plan(cfg, max_jobs=6)
+    inten, stats, psnr = plan.propagate(bits, tgt)
+    pop = (pre >= 0.5).reshape(4, 3, 8, -1).sum(dim=(2, 3)).double() / 8.0
+    s = inten.double().sum(dim=(2, 3))
+    assert torch.allclose(s, pop, rtol=2e-6)
+    # the stats' sum I^2 matches the returned intensity
+    assert torch.allclose(stats[..., 1], (inten.double() ** 2).sum(dim=(2, 3)), rtol=1e-9)
+
+
+def test_deterministic_bitwise():
+    import hbx
+    cfg = hbx.rgb_config(256)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    bits = hbx.pack_bits(torch.rand((2, 24, 256, 256), generator=g, device="cuda") >= 0.5)
+    tgt = torch.rand((2, 3, 256, 256), generator=g, device="cuda")
+    plan = hbx.Plan(cfg, max_jobs=4)   # forces two chunks
+    a = plan.propagate(bits, tgt)
+    b = plan.propagate(bits, tgt)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+
+
+def test_pack_bits_matches_oracle():
+    import hbx
+    m = (np.random.default_rng(2).random((3, 4, 128)) > 0.5).astype(np.uint8)
+    got = hbx.pack_bits(torch.from_numpy(m).cuda()).cpu().numpy().view("<u8")
+    assert np.array_equal(got, O.pack_mask(m))
+    assert np.array_equal(hbx.unpack_bits(torch.from_numpy(got.view(np.int64)).cuda(), 128).cpu().numpy(), m)
+
+
+# -- trial flips ---------------------------------------------------------------------------
+def test_eval_flips_probe_golden(golden_dir):
+    import hbx
+    from hbx import dbs
+    d = load(golden_dir, "probe_64.npz")
+    cfg = dev_cfg(small_rgb())
+    plan = hbx.Plan(cfg, max_jobs=256)
+    mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
+    res = dbs.probe(plan, mask, torch.from_numpy(d["target"]).cuda(), d["flips"], pre_model=d["pre_model"])
+    assert abs(res.base_psnr - float(d["base_psnr"])) <= PSNR_TOL
+    assert np.max(np.abs(res.psnr - d["psnr"])) <= PSNR_TOL
+    delta = d["psnr"] - d["base_psnr"]
+    clear = np.abs(delta) > 1e-5          # fp32 cannot order ties below this
+    assert np.array_equal(res.improved[clear], (delta > 0)[clear])
+    assert np.array_equal(res.attempted_bins, d["attempted"])
+    assert np.sum(np.abs(res.improved_bins - d["improved"])) <= np.sum(~clear)
+
+
+def test_eval_flips_1024_vs_oracle():
+    import hbx
+    ocfg = O.rgb_config(1024)
+    pre, tgt = O.synthetic_inputs(ocfg, 3)
+    env = O.OracleEnv(ocfg)
+    env.reset(pre, tgt)
+    flips = np.array([0, 1024 * 1024 - 1, 9 * 1024 * 1024 + 5 * 1024 + 77, 24 * 1024 * 1024 - 1], np.int64)
+    want = [env.evaluate_flip(int(a))[0] for a in flips]
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=4)
+    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    _, st, _ = plan.propagate(bits[None], torch.from_numpy(tgt).cuda()[None])
+    got, _ = plan.eval_flips(bits, torch.from_numpy(tgt).cuda(), st[0].contiguous(),
+                             torch.from_numpy(flips).cuda())
+    assert np.max(np.abs(got.cpu().numpy() - np.array(want))) <= PSNR_TOL
+
+
+# -- env semantics ---------------------------------------------------------------------------
+def test_env_trace_golden(golden_dir):
+    import hbx
+    from hbx.env import HologramVecEnv
+    d = load(golden_dir, "env_trace_64.npz")
+    ms, tp, ts, td = d["params"]
+    cfg = dev_cfg(small_rgb())
+    env = HologramVecEnv(cfg, 1, lambda i: d["target"], pre_model_source=lambda i: d["pre_model"],
+                         max_steps=int(ms), T_PSNR=float(tp), T_steps=int(ts), T_PSNR_DIFF=float(td),
+                         auto_reset=False)
+    env.reset()
+    assert abs(float(env.state.init_psnr[0]) - float(d["initial_psnr"])) <= PSNR_TOL
+    for k, a in enumerate(d["actions"]):
+        r, ps, acc, term, trunc = env.step_device(torch.tensor([int(a)], device="cuda"))
+        assert abs(float(ps[0]) - float(d["psnr"][k])) <= PSNR_TOL, k
+        assert abs(float(r[0]) - float(d["reward"][k])) <= 800 * PSNR_TOL, k
+        assert (bool(acc[0]), bool(term[0]), bool(trunc[0])) == (
+            bool(d["accepted"][k]), bool(d["terminated"][k]), bool(d["truncated"][k])), k
+    fm = env.state.mask[0].cpu().numpy().view("<u8")
+    assert np.array_equal(fm, d["final_mask_bits"])
+    assert np.array_equal(env.state.record[0].cpu().numpy(), d["final_record"])
+    assert int(env.state.steps[0]) == len(d["actions"])
+
+
+def test_vecenv_batch_matches_oracle_per_env():
+    import hbx
+    from hbx.env import HologramVecEnv
+    ocfg = small_rgb()
+    B = 6
+    ins = [O.synthetic_inputs(ocfg, 100 + b) for b in range(B)]
+    env = HologramVecEnv(dev_cfg(ocfg), B, lambda i: ins[i][1], pre_model_source=lambda i: ins[i][0],
+                         auto_reset=False)
+    env.reset()
+    oenvs = [O.OracleEnv(ocfg) for _ in range(B)]
+    for b in range(B):
+        oenvs[b].reset(*ins[b])
+    rng = np.random.default_rng(8)
+    for _ in range(25):
+        acts = rng.integers(0, ocfg.channels * 64 * 64, B)
+        r, ps, acc, term, trunc = env.step_device(torch.from_numpy(acts).cuda())
+        ps, acc = ps.cpu().numpy(), acc.cpu().numpy()
+        for b in range(B):
+            want = oenvs[b].step(int(acts[b]))
+            assert abs(ps[b] - want.psnr) <= PSNR_TOL
+            assert bool(acc[b]) == want.accepted
+
+
+def test_invalid_action_raises():
+    from hbx.env import HologramVecEnv
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 1)
+    env = HologramVecEnv(dev_cfg(ocfg), 1, lambda i: tgt, pre_model_source=lambda i: pre, auto_reset=False)
+    env.reset()
+    with pytest.raises(ValueError):
+        env.step(np.array([ocfg.channels * 64 * 64]))
+
+
+def test_vecenv_auto_reset_and_obs():
+    from hbx.env import HologramVecEnv
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 2)
+    env = HologramVecEnv(dev_cfg(ocfg), 2, lambda i: tgt, pre_model_source=lambda i: pre, max_steps=3)
+    obs = env.reset()
+    assert obs["state"].shape == (2, 1, 6, 64, 64) and obs["recon_image"].shape == (2, 1, 3, 64, 64)
+    assert np.array_equal(obs["state"][0, 0].cpu().numpy(), (pre >= 0.5).astype(np.int8))
+    seen_done = False
+    for _ in range(12):
+        obs, rew, dones, infos = env.step(np.array([5, 7]))
+        if dones.any():
+            seen_done = True
+            i = int(np.nonzero(dones)[0][0])
+            assert "terminal_observation" in infos[i]
+            assert int(env.state.steps[i]) == 0       # auto-reset happened
+    assert seen_done
+
+
+# -- DBS --------------------------------------------------------------------------------------
+def test_dbs_greedy_speculative_equals_serial(golden_dir):
+    import hbx
+    from hbx import dbs
+    d = load(golden_dir, "dbs_trace_64.npz")
+    plan = hbx.Plan(dev_cfg(small_rgb()), max_jobs=128)
+    mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
+    res = dbs.greedy(plan, mask, torch.from_numpy(d["target"]).cuda(), d["order"])
+    want_pos = np.nonzero(d["accepted"])[0]
+    assert np.array_equal(np.array(res.accepted_positions), want_pos)
+    assert abs(res.final_psnr - float(d["final_psnr"])) <= PSNR_TOL
+    assert np.array_equal(mask.cpu().numpy().view("<u8"), d["final_mask_bits"])
+    assert res.launches < len(d["order"])      # speculation batched the walk
+
+
+def test_dbs_early_stop():
+    import hbx
+    from hbx import dbs
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 21)
+    order = np.random.default_rng(3).permutation(ocfg.channels * 64 * 64)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=64)
+    mask = hbx.pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+    res = dbs.greedy(plan, mask, torch.from_numpy(tgt).cuda(), order, stop_diff=0.05)
+    env = O.OracleEnv(ocfg, accept_rule=1)
+    env.reset(pre, tgt)
+    acc, ps, final = O.dbs_greedy(env, order, stop_diff=0.05)
+    assert res.stopped_early
+    assert res.steps == len(acc)
+    assert abs(res.final_psnr - final) <= PSNR_TOL

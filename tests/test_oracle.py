@@ -1,0 +1,216 @@
+"""Oracle pinning (CPU): known answers stated by the reference, analytic
+properties of the restated physics, and the committed golden vectors.
+
+Parity note: the floating-point physics (torchOptics) is unpinned -- see the
+oracle header; these tests pin what can be pinned."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import hbx_oracle as O
+
+
+# -- known answers from the reference -------------------------------------------------
+def test_reward_cubic_known_answers():
+    # env.py:228-229: "1 = +300, 1/2 = +100, 1/4 = -100, 1/8 = -300"
+    for s, want in ((1.0, 300.0), (0.5, 100.0), (0.25, -100.0), (0.125, -300.0)):
+        assert abs(O.success_cubic(s) - want) < 0.05
+        assert abs(O.max_steps_cubic(s) - want) < 0.05
+    # exact values of the reference's literal coefficients
+    assert O.success_cubic(1.0) == pytest.approx(300.04, abs=1e-9)
+    assert O.max_steps_cubic(1.0) == pytest.approx(300.0, abs=1e-9)
+    assert O.success_cubic(0.5) == pytest.approx(100.03875, abs=1e-9)
+    assert O.success_cubic(0.125) == pytest.approx(-299.96185546875, abs=1e-9)
+
+
+@pytest.mark.parametrize("n,ch", [(256, 8), (1024, 24)])
+def test_decode_edges(n, ch):
+    hw = n * n
+    assert tuple(int(v) for v in O.decode_action(0, n, n)) == (0, 0, 0)
+    assert tuple(int(v) for v in O.decode_action(hw - 1, n, n)) == (0, n - 1, n - 1)
+    assert tuple(int(v) for v in O.decode_action(hw, n, n)) == (1, 0, 0)
+    assert tuple(int(v) for v in O.decode_action(ch * hw - 1, n, n)) == (ch - 1, n - 1, n - 1)
+    a = np.random.default_rng(0).integers(0, ch * hw, 1000)
+    c, r, col = O.decode_action(a, n, n)
+    assert np.array_equal(O.encode_action(c, r, col, n, n), a)
+
+
+def test_decode_matches_reference_formula():
+    # the literal python of env.py:158-161 on python ints
+    for a in (0, 1, 65535, 65536, 524287, 25165823, 12345678):
+        for ips in (256, 1024):
+            ch, pi = a // (ips * ips), a % (ips * ips)
+            want = (ch, pi // ips, pi % ips)
+            assert tuple(int(v) for v in O.decode_action(a, ips, ips)) == want
+
+
+def test_pack_roundtrip():
+    m = (np.random.default_rng(1).random((3, 5, 128)) > 0.5).astype(np.uint8)
+    bits = O.pack_mask(m)
+    assert bits.shape == (3, 5, 2) and bits.dtype == np.dtype("<u8")
+    assert np.array_equal(O.unpack_mask(bits, 128), m)
+    # bit j of word w is column 64 w + j
+    one = np.zeros((1, 128), np.uint8)
+    one[0, 70] = 1
+    assert O.pack_mask(one)[0, 1] == np.uint64(1 << 6)
+
+
+# -- analytic properties of the restated physics ---------------------------------------
+def test_parseval_energy_conserved():
+    cfg = O.rgb_config(64, planes=2)
+    pre, _ = O.synthetic_inputs(cfg, 5)
+    mask = (pre >= 0.5).astype(np.uint8)
+    prop = O.Propagator(cfg)
+    for g in range(3):
+        inten = prop.group_intensity(mask, g)
+        # |H| = 1 on the propagating band (no evanescent cut at these params)
+        assert np.sum(inten) == pytest.approx(mask[2 * g:2 * g + 2].sum() / 2.0, rel=1e-12)
+
+
+def test_plane_wave_invariant():
+    cfg = O.mono_config(64)
+    mask = np.ones((8, 64, 64), np.uint8)
+    inten = O.Propagator(cfg).group_intensity(mask, 0)
+    assert np.allclose(inten, 1.0, atol=1e-12)
+
+
+def test_asm_close_to_fresnel_at_small_angle():
+    h_asm = O.transfer_function(64, 64, 7.56e-6, 7.56e-6, 515e-9, 2e-3, O.TF_ASM)
+    h_fr = O.transfer_function(64, 64, 7.56e-6, 7.56e-6, 515e-9, 2e-3, O.TF_FRESNEL)
+    # identical up to the global phase and the O((lambda f)^4) term
+    ratio = h_asm / h_fr
+    ratio /= ratio[0, 0]
+    assert np.max(np.abs(np.angle(ratio))) < 0.05
+
+
+def test_transfer_function_even():
+    h = O.transfer_function(64, 64, 7.56e-6, 7.56e-6, 638e-9, 2e-3)
+    idx = (-np.arange(64)) % 64
+    assert np.allclose(h, h[idx][:, idx])
+
+
+def test_psnr_stats_identity():
+    rng = np.random.default_rng(3)
+    x = rng.random((3, 32, 32))
+    y = rng.random((3, 32, 32)).astype(np.float32)
+    st = np.stack([O.chan_stats(x[g], y[g]) for g in range(3)])
+    for rs in (O.REL_LSQ, O.REL_NONE):
+        assert O.psnr_from_stats(st, x.size, rs) == pytest.approx(O.relative_psnr(x, y, rs), abs=1e-10)
+
+
+def test_phase_field_mapping():
+    m = np.array([[0, 1]], np.uint8)
+    assert np.array_equal(O.mask_to_field(m, O.FIELD_PHASE), np.array([[1.0, -1.0]]))
+    assert np.array_equal(O.mask_to_field(m, O.FIELD_AMPLITUDE), np.array([[0.0, 1.0]]))
+
+
+# -- env semantics quirks (env.py:184-259) -----------------------------------------------
+def _small_env(**kw):
+    cfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    pre, tgt = O.synthetic_inputs(cfg, 9)
+    env = O.OracleEnv(cfg, **kw)
+    env.reset(pre, tgt)
+    return env, cfg
+
+
+def test_rollback_keeps_record_and_never_terminates():
+    env, cfg = _small_env(max_steps=3)
+    rng = np.random.default_rng(4)
+    saw_rollback_at_max = False
+    for _ in range(40):
+        a = int(rng.integers(0, cfg.channels * 64 * 64))
+        c, r, col = (int(v) for v in O.decode_action(a, 64, 64))
+        before = env.state_record[c, r, col]
+        res = env.step(a)
+        assert env.state_record[c, r, col] == np.int8(before + 1)      # record never decremented
+        if not res.accepted:
+            assert not res.terminated and not res.truncated           # early return (env.py:196)
+            if env.steps >= env.max_steps:
+                saw_rollback_at_max = True
+        else:
+            assert res.truncated == (env.steps >= 3)
+    assert saw_rollback_at_max
+
+
+def test_reward_is_800_delta_when_rejected():
+    env, cfg = _small_env()
+    prev = env.previous_psnr
+    for a in range(0, 5000, 97):
+        res = env.step(a)
+        if not res.accepted:
+            assert res.reward == pytest.approx(800.0 * (res.psnr - prev))
+        prev = env.previous_psnr
+
+
+def test_dbs_accept_strict_vs_env_nonstrict():
+    assert O.OracleEnv.__dataclass_fields__["accept_rule"].default == 0
+
+
+def test_premodel_bins():
+    assert O.premodel_bin(0.0) == 0 and O.premodel_bin(0.0999) == 0 and O.premodel_bin(0.1) == 1
+    assert O.premodel_bin(0.95) == 9 and O.premodel_bin(1.0) == 9 and O.premodel_bin(1.01) == -1
+
+
+def test_importance_ranks_threshold():
+    d = np.array([-0.1, 0.2, 0.05, -0.3, 0.4])
+    ranks, thr = O.importance_ranks(d)
+    assert thr == pytest.approx((0.2 + 0.05 + 0.4) / 4)
+    assert ranks[np.argmax(d)] == pytest.approx(np.poly1d(np.polyfit(
+        [10000, 9000, 8000, 5000, 2500, 1], [-0.5, -0.48, -0.45, -0.35, 0, 1], 5))(1.0))
+
+
+# -- golden vectors: the oracle reproduces the committed fixtures --------------------------
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name), allow_pickle=False)
+
+
+def test_golden_decode_and_reward(golden_dir):
+    t = _load(golden_dir, "decode.npz")["table"]
+    for n, ch, a, c, r, col in t:
+        assert tuple(int(v) for v in O.decode_action(a, n, n)) == (c, r, col)
+    rw = _load(golden_dir, "reward.npz")
+    for s, a, b in zip(rw["success_ratio"], rw["success_cubic"], rw["max_steps_cubic"]):
+        assert O.success_cubic(s) == a and O.max_steps_cubic(s) == b
+
+
+def test_golden_propagation(golden_dir):
+    import tests.golden.make_golden as G
+    for name, fn in (("prop_64_rgb.npz", G.small_rgb_cfg),
+                     ("prop_256_mono.npz", lambda **kw: O.mono_config(256, **kw))):
+        d = _load(golden_dir, name)
+        mask = O.unpack_mask(d["mask_bits"], d["target"].shape[-1])
+        for i, (tf, fk, rs) in enumerate(d["combos"]):
+            if i > 1 and name.startswith("prop_256"):
+                break   # keep the CPU suite fast; the GPU tests cover every combo
+            c = fn(tf_kind=int(tf), field_kind=int(fk), rel_scale=int(rs))
+            prop = O.Propagator(c)
+            inten = prop.all_intensity(mask)
+            st = np.stack([O.chan_stats(inten[g], d["target"][g]) for g in range(c.groups)])
+            assert np.allclose(st, d["stats"][i], rtol=1e-12, atol=1e-9)
+            assert prop.psnr(st) == pytest.approx(float(d["psnr"][i]), abs=1e-10)
+
+
+def test_golden_env_trace(golden_dir):
+    d = _load(golden_dir, "env_trace_64.npz")
+    cfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    ms, tp, ts, td = d["params"]
+    env = O.OracleEnv(cfg, max_steps=int(ms), T_PSNR=float(tp), T_steps=int(ts), T_PSNR_DIFF=float(td))
+    assert env.reset(d["pre_model"], d["target"]) == pytest.approx(float(d["initial_psnr"]), abs=1e-10)
+    for k, a in enumerate(d["actions"][:60]):
+        r = env.step(int(a))
+        assert r.psnr == pytest.approx(float(d["psnr"][k]), abs=1e-10)
+        assert r.reward == pytest.approx(float(d["reward"][k]), abs=1e-7)
+        assert (r.accepted, r.terminated, r.truncated) == (
+            bool(d["accepted"][k]), bool(d["terminated"][k]), bool(d["truncated"][k]))
+
+
+def test_golden_dbs_prefix(golden_dir):
+    d = _load(golden_dir, "dbs_trace_64.npz")
+    cfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    env = O.OracleEnv(cfg, accept_rule=1)
+    env.reset(d["pre_model"], d["target"])
+    acc, ps, _ = O.dbs_greedy(env, d["order"][:300])
+    assert np.array_equal(acc, d["accepted"][:300])
+    assert np.allclose(ps, d["psnr"][:300], atol=1e-10)
