@@ -229,8 +229,9 @@ def test_vecenv_auto_reset_and_obs():
     assert obs["state"].shape == (2, 1, 6, 64, 64) and obs["recon_image"].shape == (2, 1, 3, 64, 64)
     assert np.array_equal(obs["state"][0, 0].cpu().numpy(), (pre >= 0.5).astype(np.int8))
     seen_done = False
-    for _ in range(12):
-        obs, rew, dones, infos = env.step(np.array([5, 7]))
+    rng = np.random.default_rng(0)
+    for _ in range(40):
+        obs, rew, dones, infos = env.step(rng.integers(0, 6 * 4096, 2))
         if dones.any():
             seen_done = True
             i = int(np.nonzero(dones)[0][0])
