@@ -159,8 +159,6 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_HIP, "table upload");
-  size_t lds = 0;
-  if (hbx::col_kernel_lds(R, &lds) != hipSuccess) return cleanup(HBX_ERR_HIP, "column kernel LDS attribute");
   *out = p;
   return HBX_OK;
 }

@@ -146,6 +146,9 @@ struct ColumnScratch {
 // tw: LDS table [k1][t] = W_N^{t k1} (forward sign).
 template <int R, bool INV, class Scratch>
 __device__ __forceinline__ void fft_group(float2 (&v)[R], int t, const Scratch& sc, const float2* tw) {
+  // keep the twiddle loads local to each FFT: without this barrier the
+  // compiler CSEs / hoists them across calls and pins 2R VGPRs for good
+  asm volatile("" ::: "memory");
   dft_reg<R, INV>(v);
 #pragma unroll
   for (int k1 = 1; k1 < R; ++k1) {

@@ -68,7 +68,6 @@ struct EnvParams {
 
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, hipStream_t st);
-hipError_t col_kernel_lds(int R, size_t* bytes);
 hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W, int P, int CH,
                                     JobDesc* jobs, int32_t* err, hipStream_t st);
 hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int P, int CH,

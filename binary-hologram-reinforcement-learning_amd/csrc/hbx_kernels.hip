@@ -1,20 +1,8 @@
 // hbx_kernels.hip -- HIP kernels of the binary-hologram hot path (gfx950).
 //
-// One "job" = one colour group (P planes, N x N) of one env propagated with an
-// optional single-pixel flip applied on the fly.  A job runs through three
-// passes over a per-job workspace ws[job][P][N][N] (complex64, in place):
-//
-//   k_rowfwd  bits -> real row FFTs, two planes packed into one complex FFT,
-//             Hermitian split, half spectrum (kx < N/2; Nyquist packed into
-//             the imaginary part of kx = 0)                          [write N^2/2]
-//   k_col     per strip of SW half-spectrum columns (LDS [N][SW+1]):
-//             column FFT -> x H(kx,ky) (and the mirrored column N-kx
-//             through Hermitian symmetry) -> two inverse column FFTs [read N^2/2, write N^2]
-//   k_rowinv  per row, all P planes: inverse row FFT, |U|^2, plane mean,
-//             f64 partial sums (I*T, I^2, T^2) against the target   [read N^2 + target]
-//
-// then tiny per-env kernels turn the partial sums into PSNR / reward /
-// accept-rollback (env.py:154-259) on the device -- no host sync per step.
+// This file: the small per-job / per-env kernels that turn the propagation
+// passes' partial sums (hbx_passes.hip) into PSNR / reward / accept-rollback
+// (env.py:154-259) on the device -- no host sync per step.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -23,264 +11,6 @@
 #include "hbx_internal.hpp"
 
 namespace hbx {
-
-// ---------------------------------------------------------------------------
-// Pass 1: forward row FFT of two bit-planes (real) packed as one complex FFT.
-// Block = 256 threads = 256/R lane groups; group -> (job, plane pair, row).
-// ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(256) void k_rowfwd(const JobDesc* __restrict__ jobs,
-                                                const uint32_t* __restrict__ mask,
-                                                float2* __restrict__ ws,
-                                                const float2* __restrict__ tw_glob, int P,
-                                                int CH, float va, float vb) {
-  constexpr int N = R * R;
-  constexpr int GPB = 256 / R;     // lane groups (rows) per block
-  constexpr int WPR = N / 32;      // 32-bit words per mask row
-  __shared__ float2 tw[N];
-  __shared__ float2 scratch[GPB * R * (R + 1)];
-
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
-  __syncthreads();
-
-  const int grp = threadIdx.x / R;
-  const int t = threadIdx.x % R;
-  const int lane_base = (threadIdx.x & 63) - t;
-  constexpr int RB = N / GPB;     // row blocks per plane pair
-  int bid = blockIdx.x;
-  const int rb = bid % RB;
-  bid /= RB;
-  const int q = bid % (P / 2);
-  const int j = bid / (P / 2);
-  const JobDesc jb = jobs[j];
-  if (jb.env < 0) return;  // invalid job (uniform per block)
-  const int y = rb * GPB + grp;
-  const int pa = 2 * q, pb = 2 * q + 1;
-  const int ca = jb.group * P + pa;
-
-  const uint32_t* rowa = mask + ((size_t)jb.env * CH + ca) * N * WPR + (size_t)y * WPR;
-  const uint32_t* rowb = rowa + (size_t)N * WPR;
-  uint32_t wa[WPR], wb[WPR];
-  if constexpr (WPR % 4 == 0) {
-#pragma unroll
-    for (int i = 0; i < WPR / 4; ++i) {
-      const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
-      const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
-      wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
-      wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < WPR; ++i) { wa[i] = rowa[i]; wb[i] = rowb[i]; }
-  }
-  // on-the-fly single-pixel flip of this job (env.py:164)
-  if (jb.flip_plane >= 0 && jb.flip_pix / N == y) {
-    const int col = jb.flip_pix % N;
-    const uint32_t bit = 1u << (col & 31);
-#pragma unroll
-    for (int i = 0; i < WPR; ++i) {
-      if (i == (col >> 5)) {
-        if (jb.flip_plane == pa) wa[i] ^= bit;
-        if (jb.flip_plane == pb) wb[i] ^= bit;
-      }
-    }
-  }
-  float2 v[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) {
-    const int w = (R * jj) >> 5;
-    const int sh = ((R * jj) & 31) + t;
-    v[jj].x = fmaf(vb, (float)((wa[w] >> sh) & 1u), va);
-    v[jj].y = fmaf(vb, (float)((wb[w] >> sh) & 1u), va);
-  }
-  PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
-  fft_group<R, false>(v, t, sc, tw);
-
-  // Hermitian split: F_a = (Z + conj Z(-k))/2, F_b = -i (Z - conj Z(-k))/2
-  float2* outa = ws + (((size_t)j * P + pa) * N + y) * N;
-  float2* outb = outa + (size_t)N * N;
-  const float2 zny = v[R / 2];  // Z[N/2] on lane 0
-#pragma unroll
-  for (int k2 = 0; k2 < R / 2; ++k2) {
-    const float2 z = v[k2];
-    const float2 m = mirror_conj<R>(v, k2, t, lane_base);
-    float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-    float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
-    if (k2 == 0 && t == 0) {  // DC and Nyquist are real: pack Nyquist in .y
-      fa = make_float2(z.x, zny.x);
-      fb = make_float2(z.y, zny.y);
-    }
-    outa[t + R * k2] = fa;
-    outb[t + R * k2] = fb;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pass 2: column pass on a strip of SW = 256/R half-spectrum columns.
-// ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(256) void k_col(const JobDesc* __restrict__ jobs,
-                                             float2* __restrict__ ws,
-                                             const float2* __restrict__ htab,
-                                             const float2* __restrict__ tw_glob, int P) {
-  constexpr int N = R * R;
-  constexpr int SW = 256 / R;         // columns per strip
-  constexpr int PITCH = SW + 1;
-  constexpr int NSTRIP = (N / 2) / SW;
-  extern __shared__ __attribute__((aligned(16))) float2 smem[];
-  float2* tw = smem;                  // [N]
-  float2* strip = smem + N;           // [N][PITCH]
-
-  int bid = blockIdx.x;
-  const int s = bid % NSTRIP;
-  bid /= NSTRIP;
-  const int p = bid % P;
-  const int j = bid / P;
-  const JobDesc jb = jobs[j];
-  if (jb.env < 0) return;
-  const int x0 = s * SW;
-  float2* plane = ws + ((size_t)j * P + p) * N * N;
-
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
-  for (int i = threadIdx.x; i < N * SW; i += 256) {
-    const int yy = i / SW, c = i % SW;
-    strip[yy * PITCH + c] = plane[(size_t)yy * N + x0 + c];
-  }
-  __syncthreads();
-
-  const int c = threadIdx.x / R;
-  const int t = threadIdx.x % R;
-  const int lane_base = (threadIdx.x & 63) - t;
-  const int kx = x0 + c;
-  float2 v[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) v[jj] = strip[(t + R * jj) * PITCH + c];
-  ColumnScratch<R, PITCH> sc{strip + c};
-  fft_group<R, false>(v, t, sc, tw);
-
-  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N;
-  // kx != 0: G(kx) = F H(kx), G(N-kx) = conj F(kx,-ky) H(kx)   (H even in fx)
-  // kx == 0: the packed column z = F(0,y) + i F(N/2,y) (both real sequences)
-  //          splits into F(0) = (Z + M)/2 and F(N/2) = -i (Z - M)/2.
-  // Branch-free so the lane shuffles never run under divergent control flow.
-  const bool dc = (kx == 0);
-  const float2* h1p = hg + (dc ? 0 : (size_t)kx * N);
-  const float2* h2p = dc ? hg + (size_t)(N / 2) * N : h1p;
-  float2 g1[R], g2[R];
-#pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) {
-    const float2 z = v[k2];
-    const float2 m = mirror_conj<R>(v, k2, t, lane_base);
-    const float2 a1 = dc ? make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y)) : z;
-    const float2 a2 = dc ? make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x)) : m;
-    g1[k2] = cmul(a1, h1p[t + R * k2]);
-    g2[k2] = cmul(a2, h2p[t + R * k2]);
-  }
-  fft_group<R, true>(g1, t, sc, tw);
-  fft_group<R, true>(g2, t, sc, tw);
-
-  // direct columns: kx -> kx
-#pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) strip[(t + R * k2) * PITCH + c] = g1[k2];
-  __syncthreads();
-  for (int i = threadIdx.x; i < N * SW; i += 256) {
-    const int yy = i / SW, cc = i % SW;
-    plane[(size_t)yy * N + x0 + cc] = strip[yy * PITCH + cc];
-  }
-  __syncthreads();
-  // mirrored columns: kx -> N - kx (kx = 0 -> N/2)
-#pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) strip[(t + R * k2) * PITCH + c] = g2[k2];
-  __syncthreads();
-  for (int i = threadIdx.x; i < N * SW; i += 256) {
-    const int yy = i / SW, cc = i % SW;
-    const int kk = x0 + cc;
-    const int xm = (kk == 0) ? (N / 2) : (N - kk);
-    plane[(size_t)yy * N + xm] = strip[yy * PITCH + cc];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pass 3: inverse row FFT of all P planes of a row, |U|^2 plane mean and
-// f64 partial sums against the target row.
-// ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(256) void k_rowinv(const JobDesc* __restrict__ jobs,
-                                                const float2* __restrict__ ws,
-                                                const float* __restrict__ target,
-                                                const float2* __restrict__ tw_glob, int P, int G,
-                                                double* __restrict__ partial,
-                                                float* __restrict__ inten_out) {
-  constexpr int N = R * R;
-  constexpr int GPB = 256 / R;
-  constexpr int RB = N / GPB;
-  __shared__ float2 tw[N];
-  __shared__ float2 scratch[GPB * R * (R + 1)];
-  __shared__ double red[GPB][3];
-
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
-  __syncthreads();
-
-  const int grp = threadIdx.x / R;
-  const int t = threadIdx.x % R;
-  const int rb = blockIdx.x % RB;
-  const int j = blockIdx.x / RB;
-  const JobDesc jb = jobs[j];
-  if (jb.env < 0) {
-    if (threadIdx.x == 0) {
-      double* o = partial + ((size_t)j * RB + rb) * 3;
-      o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
-    }
-    return;
-  }
-  const int y = rb * GPB + grp;
-  PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
-
-  float acc[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) acc[k] = 0.0f;
-  for (int p = 0; p < P; ++p) {
-    const float2* row = ws + (((size_t)j * P + p) * N + y) * N;
-    float2 v[R];
-#pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = row[t + R * jj];
-    fft_group<R, true>(v, t, sc, tw);
-#pragma unroll
-    for (int k = 0; k < R; ++k) acc[k] += norm2(v[k]);
-  }
-  const float invp = 1.0f / (float)P;
-  const float* trow = target + (((size_t)jb.env * G + jb.group) * N + y) * N;
-  double sxy = 0.0, sxx = 0.0, syy = 0.0;
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const float I = acc[k] * invp;
-    const float T = trow[t + R * k];
-    sxy = fma((double)I, (double)T, sxy);
-    sxx = fma((double)I, (double)I, sxx);
-    syy = fma((double)T, (double)T, syy);
-    acc[k] = I;
-  }
-  if (inten_out) {
-    float* orow = inten_out + ((size_t)j * N + y) * N;
-#pragma unroll
-    for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
-  }
-  // reduce over the R lanes of the group (fixed butterfly order -> deterministic)
-#pragma unroll
-  for (int off = R / 2; off >= 1; off >>= 1) {
-    sxy += __shfl_xor(sxy, off, 64);
-    sxx += __shfl_xor(sxx, off, 64);
-    syy += __shfl_xor(syy, off, 64);
-  }
-  if (t == 0) { red[grp][0] = sxy; red[grp][1] = sxx; red[grp][2] = syy; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0, cc = 0.0;
-    for (int g = 0; g < GPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
-    double* o = partial + ((size_t)j * RB + rb) * 3;
-    o[0] = a; o[1] = b; o[2] = cc;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Small per-job / per-env kernels
@@ -575,71 +305,6 @@ __global__ void k_psnr(const double* __restrict__ chan_stats, int n, int G, doub
     sxy += s[0]; sxx += s[1]; syy += s[2];
   }
   psnr[b] = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
-}
-
-// ---------------------------------------------------------------------------
-// Host-side launch helpers (called from hbx_api.cpp)
-// ---------------------------------------------------------------------------
-template <int R>
-static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jobs,
-                                const uint32_t* mask, const float* target, float* inten_out,
-                                hipStream_t st) {
-  constexpr int N = R * R;
-  constexpr int GPB = 256 / R;
-  constexpr int SW = 256 / R;
-  const int P = pd.P;
-  const int CH = pd.G * pd.P;
-  PassTimer* tm = pd.timer;
-  {
-    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / GPB);
-    if (tm) tm->begin(0, st);
-    hipLaunchKernelGGL(k_rowfwd<R>, dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws, pd.tw, P,
-                       CH, pd.va, pd.vb);
-    if (tm) tm->end(0, n_jobs, st);
-  }
-  {
-    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / SW);
-    const size_t lds = (size_t)(N + N * (SW + 1)) * sizeof(float2);
-    if (tm) tm->begin(1, st);
-    hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), lds, st, jobs, pd.ws, pd.htab, pd.tw, P);
-    if (tm) tm->end(1, n_jobs, st);
-  }
-  {
-    const unsigned blocks = (unsigned)n_jobs * (N / GPB);
-    if (tm) tm->begin(2, st);
-    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws, target, pd.tw,
-                       P, pd.G, pd.partial, inten_out);
-    if (tm) tm->end(2, n_jobs, st);
-  }
-  {
-    const int RB = N / GPB;
-    hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial,
-                       n_jobs, RB, pd.job_stats);
-  }
-  return hipGetLastError();
-}
-
-hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
-                    const float* target, float* inten_out, hipStream_t st) {
-  switch (pd.R) {
-    case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, st);
-    case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, st);
-    case 8: return launch_passes<8>(pd, jobs, n_jobs, mask, target, inten_out, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t col_kernel_lds(int R, size_t* bytes) {
-  const int N = R * R, SW = 256 / R;
-  *bytes = (size_t)(N + N * (SW + 1)) * sizeof(float2);
-  hipError_t e = hipSuccess;
-  switch (R) {
-    case 32: e = hipFuncSetAttribute((const void*)k_col<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)*bytes); break;
-    case 16: e = hipFuncSetAttribute((const void*)k_col<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)*bytes); break;
-    case 8: e = hipFuncSetAttribute((const void*)k_col<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)*bytes); break;
-    default: return hipErrorInvalidValue;
-  }
-  return e;
 }
 
 hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W, int P, int CH,

@@ -1,0 +1,384 @@
+// hbx_passes.hip -- the three propagation passes (gfx950, wave64).
+//
+// One "job" = one colour group (P planes, N x N) of one env, propagated with
+// an optional single-pixel flip applied on the fly (env.py:164-172).  Per job
+// the workspace ws[job][P][N][N] complex64 is used in place, COLUMN-MAJOR:
+// line kx holds the N values over y, so the heavy column pass streams whole
+// contiguous lines and the two transposes a 2-D FFT needs live in LDS tiles of
+// the row passes.
+//
+//   k_rowfwd  GPB rows of a plane pair per block: bits -> one complex FFT per
+//             row pair (plane a real, plane b imaginary) -> Hermitian split ->
+//             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0) ->
+//             LDS tile transpose -> A[kx][y0..y0+GPB)        [HBM: read N^2/8 B, write 4 N^2 B per plane]
+//   k_col     per half-spectrum line kx, two lane groups: FFT over y ->
+//             x H(kx, ky) -> IFFT -> line kx, and (Hermitian symmetry)
+//             conj F(kx, -ky) H(kx, ky) -> IFFT -> line N - kx (N/2 for
+//             kx = 0)                                                  [read 4 N^2, write 8 N^2]
+//   k_rowinv  GPB rows per block, all P planes: LDS tile transpose of
+//             B[kx][y0..y0+GPB) -> IFFT over kx -> |U|^2 -> plane mean ->
+//             f64 partials of (I*T, I^2, T^2) against the target row  [read 8 N^2 per plane + 4 N^2]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbx_fft.hpp"
+#include "hbx_internal.hpp"
+
+namespace hbx {
+
+// Position of element (line, r) in an LDS tile [line][GPB rows], r XOR-swizzled
+// by a function of (line mod R) only: lane t of a group reading line t + R*j
+// then addresses base_t + j*R*GPB (immediate offsets, no per-j address VGPRs),
+// ds_read_b64 is conflict-free and ds_write_b64 at most 2-way (checked
+// exhaustively for R = 8, 16, 32).
+template <int R>
+__device__ __forceinline__ int tile_pos(int line, int r) {
+  constexpr int GPB = 256 / R;
+  constexpr int SR = ilog2c(32 / GPB);
+  constexpr int SL = ilog2c(GPB / 8);
+  return line * GPB + (r ^ ((((line & (R - 1)) >> SR) << SL) & (GPB - 1)));
+}
+
+// ---------------------------------------------------------------------------
+// Pass 1
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ jobs,
+                                                   const uint32_t* __restrict__ mask,
+                                                   float2* __restrict__ ws,
+                                                   const float2* __restrict__ tw_glob, int P,
+                                                   int CH, float va, float vb) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;          // rows per block
+  constexpr int WPR = N / 32;           // 32-bit mask words per row
+  constexpr int SCR = GPB * R * (R + 1);
+  static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
+  __shared__ float2 tw[N];
+  __shared__ __attribute__((aligned(16))) float2 lds[SCR];
+
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  const int lane_base = (threadIdx.x & 63) - t;
+  constexpr int RB = N / GPB;
+  int bid = blockIdx.x;
+  const int rb = bid % RB;
+  bid /= RB;
+  const int q = bid % (P / 2);
+  const int j = bid / (P / 2);
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;  // uniform per block
+  const int y0 = rb * GPB;
+  const int y = y0 + grp;
+  const int pa = 2 * q, pb = 2 * q + 1;
+
+  const uint32_t* rowa = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR + (size_t)y * WPR;
+  const uint32_t* rowb = rowa + (size_t)N * WPR;
+  uint32_t wa[WPR], wb[WPR];
+  if constexpr (WPR % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < WPR / 4; ++i) {
+      const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
+      const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
+      wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
+      wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WPR; ++i) { wa[i] = rowa[i]; wb[i] = rowb[i]; }
+  }
+  if (jb.flip_plane >= 0 && jb.flip_pix / N == y) {  // env.py:164 flip, on the fly
+    const int col = jb.flip_pix % N;
+    const uint32_t bit = 1u << (col & 31);
+#pragma unroll
+    for (int i = 0; i < WPR; ++i) {
+      if (i == (col >> 5)) {
+        if (jb.flip_plane == pa) wa[i] ^= bit;
+        if (jb.flip_plane == pb) wb[i] ^= bit;
+      }
+    }
+  }
+  float2 v[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const int w = (R * jj) >> 5;
+    const int sh = ((R * jj) & 31) + t;
+    v[jj].x = fmaf(vb, (float)((wa[w] >> sh) & 1u), va);
+    v[jj].y = fmaf(vb, (float)((wb[w] >> sh) & 1u), va);
+  }
+  __syncthreads();  // tw visible
+  fft_group<R, false>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
+  __syncthreads();  // every group is done with its scratch: reuse as the tile
+
+  // Hermitian split -> tile[plane][kx][row]
+  float2* tile = lds;
+  const float2 zny = v[R / 2];  // Z[N/2] on lane 0
+#pragma unroll
+  for (int k2 = 0; k2 < R / 2; ++k2) {
+    const float2 z = v[k2];
+    const float2 m = mirror_conj<R>(v, k2, t, lane_base);
+    float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
+    float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+    if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
+      fa = make_float2(z.x, zny.x);
+      fb = make_float2(z.y, zny.y);
+    }
+    const int kx = t + R * k2;
+    tile[tile_pos<R>(kx, grp)] = fa;
+    tile[tile_pos<R>(N / 2 + kx, grp)] = fb;
+  }
+  __syncthreads();
+  // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
+  float2* base = ws + ((size_t)j * P + pa) * N * N;
+  constexpr int CHUNKS = N * GPB / 2;
+  static_assert(CHUNKS % 256 == 0, "chunking");
+#pragma unroll
+  for (int i = 0; i < CHUNKS / 256; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int r2 = (c % (GPB / 2)) * 2;
+    const int line = c / (GPB / 2);  // pl * N/2 + kx
+    const float2 a = tile[tile_pos<R>(line, r2)];
+    const float2 b = tile[tile_pos<R>(line, r2 + 1)];
+    const int pl = line / (N / 2), kx = line % (N / 2);
+    *reinterpret_cast<float4*>(base + (size_t)pl * N * N + (size_t)kx * N + y0 + r2) =
+        make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2
+// ---------------------------------------------------------------------------
+// Block = 8 lane groups = LPB lines x 2 roles (waves 0..W/2-1 role 1, the
+// rest role 2, so the role is uniform per wave).  Both roles FFT the same
+// input line (the second read hits L2); role 1 writes line kx, role 2 the
+// mirrored line.  One R-value array per lane: no spills at R = 32.
+//   role 1: G = a1 H(kx),  a1 = Z            (kx != 0)   a1 = (Z + M)/2     (kx == 0)
+//   role 2: G = a2 H(kx),  a2 = M            (kx != 0)   a2 = -i (Z - M)/2, H(N/2, .)  (kx == 0)
+// with Z = F(kx, ky), M = conj F(kx, -ky) (H is even in fx: H(N-kx) = H(kx)).
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs,
+                                                float2* __restrict__ ws,
+                                                const float2* __restrict__ htab,
+                                                const float2* __restrict__ tw_glob, int P) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;          // lane groups per block
+  constexpr int LPB = GPB / 2;          // lines per block
+  constexpr int LB = (N / 2) / LPB;
+  static_assert(GPB % 2 == 0 && (64 / R) <= LPB, "role must be wave-uniform");
+  __shared__ float2 tw[N];
+  __shared__ float2 scratch[GPB * R * (R + 1)];
+
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  const int role2 = grp >= LPB;
+  int bid = blockIdx.x;
+  const int lb = bid % LB;
+  bid /= LB;
+  const int p = bid % P;
+  const int j = bid / P;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;
+  const int kx = lb * LPB + (grp % LPB);
+  float2* plane = ws + ((size_t)j * P + p) * N * N;
+  const float2* in = plane + (size_t)kx * N;
+
+  float2 v[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) v[jj] = in[t + R * jj];
+  // tw visible, and EVERY group's input loads have landed before any group
+  // stores: role 1 overwrites line kx, which role 2 reads (in-place pass)
+  __syncthreads();
+  const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+  fft_group<R, false>(v, t, sc, tw);
+
+  // F (natural order: lane t, register k2 -> ky = t + R k2) into the scratch,
+  // then M[k2] = conj F(-ky) read back from lane (R - t) mod R.
+  wave_sync();
+#pragma unroll
+  for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
+  wave_sync();
+  const bool dc = (kx == 0);
+  // a = alpha Z + beta M (complex per-lane coefficients: branch-free)
+  float2 alpha, beta;
+  if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
+                beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
+  else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
+                beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
+  const float2* hp = htab + (size_t)jb.group * (N / 2 + 1) * N + (size_t)((role2 && dc) ? N / 2 : kx) * N;
+  const int tm = (R - t) & (R - 1);
+#pragma unroll
+  for (int k2 = 0; k2 < R; ++k2) {
+    // conj F(N - ky): lane tm, register R-1-k2 (lane 0: its own register (R-k2) mod R)
+    const float2 mm = (t == 0) ? *sc.at(0, (R - k2) & (R - 1)) : *sc.at(tm, R - 1 - k2);
+    const float2 m = conjf2(mm);
+    const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, m));
+    v[k2] = cmul(a, hp[t + R * k2]);
+  }
+  fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: M reads are done
+  float2* out = plane + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
+#pragma unroll
+  for (int k2 = 0; k2 < R; ++k2) out[t + R * k2] = v[k2];
+}
+
+// ---------------------------------------------------------------------------
+// Pass 3
+// ---------------------------------------------------------------------------
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ jobs,
+                                                   const float2* __restrict__ ws,
+                                                   const float* __restrict__ target,
+                                                   const float2* __restrict__ tw_glob, int P,
+                                                   int G, double* __restrict__ partial,
+                                                   float* __restrict__ inten_out) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;          // rows per block
+  constexpr int RB = N / GPB;
+  constexpr int CH16 = N * GPB / 2;     // 16-B chunks per plane tile
+  constexpr int PER = CH16 / 256;
+  static_assert(CH16 % 256 == 0, "chunking");
+  __shared__ float2 tw[N];
+  constexpr int SCR = GPB * R * (R + 1);   // padded transpose scratch reuses the tile
+  __shared__ __attribute__((aligned(16))) float2 tile[SCR > N * GPB ? SCR : N * GPB];
+  __shared__ double red[GPB][3];
+
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  const int rb = blockIdx.x % RB;
+  const int j = blockIdx.x / RB;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) {
+    if (threadIdx.x == 0) {
+      double* o = partial + ((size_t)j * RB + rb) * 3;
+      o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
+    }
+    return;
+  }
+  const int y0 = rb * GPB;
+  const int y = y0 + grp;
+  const float2* jbase = ws + (size_t)j * P * N * N;
+
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) acc[k] = 0.0f;
+
+#pragma unroll 1
+  for (int p = 0; p < P; ++p) {
+    const float2* pb = jbase + (size_t)p * N * N;
+    float4 pre[PER];   // all of this thread's tile loads in flight at once
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
+      pre[i] = *reinterpret_cast<const float4*>(pb + (size_t)line * N + y0 + r2);
+    }
+    __syncthreads();  // previous plane's scratch use is over
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
+      tile[tile_pos<R>(line, r2)] = make_float2(pre[i].x, pre[i].y);
+      tile[tile_pos<R>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
+    }
+    __syncthreads();
+    float2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const int kx = t + R * jj;
+      v[jj] = tile[tile_pos<R>(kx, grp)];
+    }
+    __syncthreads();  // tile consumed: reuse it as transpose scratch
+    fft_group<R, true>(v, t, PaddedScratch<R>{tile + grp * R * (R + 1)}, tw);
+#pragma unroll
+    for (int k = 0; k < R; ++k) acc[k] += norm2(v[k]);
+  }
+
+  const float invp = 1.0f / (float)P;
+  const float* trow = target + (((size_t)jb.env * G + jb.group) * N + y) * N;
+  double sxy = 0.0, sxx = 0.0, syy = 0.0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const float I = acc[k] * invp;
+    const float T = trow[t + R * k];
+    sxy = fma((double)I, (double)T, sxy);
+    sxx = fma((double)I, (double)I, sxx);
+    syy = fma((double)T, (double)T, syy);
+    acc[k] = I;
+  }
+  if (inten_out) {
+    float* orow = inten_out + ((size_t)j * N + y) * N;
+#pragma unroll
+    for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
+  }
+  // reduce over the R lanes of the group, fixed order -> bitwise reproducible
+#pragma unroll
+  for (int off = R / 2; off >= 1; off >>= 1) {
+    sxy += __shfl_xor(sxy, off, 64);
+    sxx += __shfl_xor(sxx, off, 64);
+    syy += __shfl_xor(syy, off, 64);
+  }
+  if (t == 0) { red[grp][0] = sxy; red[grp][1] = sxx; red[grp][2] = syy; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, cc = 0.0;
+    for (int g = 0; g < GPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
+    double* o = partial + ((size_t)j * RB + rb) * 3;
+    o[0] = a; o[1] = b; o[2] = cc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launch sequence for one batch of jobs
+// ---------------------------------------------------------------------------
+__global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,
+                                  double* __restrict__ job_stats);
+
+template <int R>
+static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jobs,
+                                const uint32_t* mask, const float* target, float* inten_out,
+                                hipStream_t st) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;
+  const int P = pd.P;
+  const int CH = pd.G * pd.P;
+  PassTimer* tm = pd.timer;
+  {
+    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / GPB);
+    if (tm) tm->begin(0, st);
+    hipLaunchKernelGGL(k_rowfwd<R>, dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws, pd.tw, P,
+                       CH, pd.va, pd.vb);
+    if (tm) tm->end(0, n_jobs, st);
+  }
+  {
+    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / (GPB / 2));
+    if (tm) tm->begin(1, st);
+    hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws, pd.htab, pd.tw, P);
+    if (tm) tm->end(1, n_jobs, st);
+  }
+  {
+    const unsigned blocks = (unsigned)n_jobs * (N / GPB);
+    if (tm) tm->begin(2, st);
+    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws, target, pd.tw,
+                       P, pd.G, pd.partial, inten_out);
+    if (tm) tm->end(2, n_jobs, st);
+  }
+  hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial,
+                     n_jobs, N / GPB, pd.job_stats);
+  return hipGetLastError();
+}
+
+hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
+                    const float* target, float* inten_out, hipStream_t st) {
+  switch (pd.R) {
+    case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, st);
+    case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, st);
+    case 8: return launch_passes<8>(pd, jobs, n_jobs, mask, target, inten_out, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace hbx
