@@ -41,6 +41,8 @@ def parse():
                     help="env-steps of the numpy oracle timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-psnr-check", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="jobs per launch sequence (0 = all envs at once)")
     return ap.parse_args()
 
 
@@ -129,7 +131,7 @@ def main():
         return torch.rand((CH, N, N), generator=g, device="cuda")
 
     vec = HologramVecEnv(cfg, B, target_source, pre_model_source=pre_model_source, obs_keys=(),
-                         auto_reset=False, max_steps=10 ** 9)
+                         auto_reset=False, max_steps=10 ** 9, max_jobs=args.chunk or None)
     vec.reset()
     gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
     n_act = CH * N * N
@@ -145,7 +147,8 @@ def main():
     for k in range(args.warmup):
         one_step(k)
     torch.cuda.synchronize()
-    vec.plan.set_timing(args.steps + 1)
+    per_step_launches = -(-B // (args.chunk or B))
+    vec.plan.set_timing(args.steps * per_step_launches + 1)
     hd.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -139,14 +139,17 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       }
     }
   const int RB = N / (256 / R);
-  p->ws_bytes = (size_t)max_jobs * P * N * N * sizeof(float2);
+  const size_t ws_a_bytes = (size_t)max_jobs * P * (N / 2) * N * sizeof(float2);
+  const size_t ws_b_bytes = (size_t)max_jobs * P * N * N * sizeof(float2);
+  p->ws_bytes = ws_a_bytes + ws_b_bytes;
   auto cleanup = [&](int code, const std::string& msg) {
     hbx_plan_destroy(p);
     return fail(code, msg);
   };
   if (hipMalloc(&pd.tw, tw.size() * sizeof(float2)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "tw");
   if (hipMalloc(&pd.htab, ht.size() * sizeof(float2)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "htab");
-  if (hipMalloc(&pd.ws, p->ws_bytes) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "workspace");
+  if (hipMalloc(&pd.ws_a, ws_a_bytes) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "workspace A");
+  if (hipMalloc(&pd.ws_b, ws_b_bytes) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "workspace B");
   if (hipMalloc(&pd.partial, (size_t)max_jobs * RB * 3 * sizeof(double)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "partial");
   if (hipMalloc(&pd.job_stats, (size_t)max_jobs * 3 * sizeof(double)) != hipSuccess)
@@ -168,7 +171,8 @@ int hbx_plan_destroy(hbx_plan_t p) {
   (void)hipSetDevice(p->device);
   if (p->pd.tw) (void)hipFree(p->pd.tw);
   if (p->pd.htab) (void)hipFree(p->pd.htab);
-  if (p->pd.ws) (void)hipFree(p->pd.ws);
+  if (p->pd.ws_a) (void)hipFree(p->pd.ws_a);
+  if (p->pd.ws_b) (void)hipFree(p->pd.ws_b);
   if (p->pd.partial) (void)hipFree(p->pd.partial);
   if (p->pd.job_stats) (void)hipFree(p->pd.job_stats);
   if (p->jobs) (void)hipFree(p->jobs);

@@ -125,6 +125,14 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier that orders LDS only: outstanding GLOBAL loads (register
+// prefetches) stay in flight across it, unlike __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Scratch layout for the transpose: a padded [R][R+1] tile private to a lane group.
 template <int R>
 struct PaddedScratch {

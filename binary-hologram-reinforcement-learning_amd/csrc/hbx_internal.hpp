@@ -38,7 +38,8 @@ struct PlanDev {
   float va, vb;        // field = va + vb * bit
   float2* tw;          // [N]  W_N^{t k1} at [k1 * R + t]
   float2* htab;        // [G][N/2 + 1][N]  H(kx, ky) / N^2
-  float2* ws;          // [max_jobs][P][N][N]
+  float2* ws_a;        // [max_jobs][P][N/2][N]  half spectrum after k_rowfwd (line kx, over y)
+  float2* ws_b;        // [max_jobs][P][N][N]    after k_col (line kx, over y)
   double* partial;     // [max_jobs][N / (256/R)][3]
   double* job_stats;   // [max_jobs][3]
   PassTimer* timer;    // nullable

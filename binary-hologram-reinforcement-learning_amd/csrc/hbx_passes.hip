@@ -1,23 +1,25 @@
 // hbx_passes.hip -- the three propagation passes (gfx950, wave64).
 //
 // One "job" = one colour group (P planes, N x N) of one env, propagated with
-// an optional single-pixel flip applied on the fly (env.py:164-172).  Per job
-// the workspace ws[job][P][N][N] complex64 is used in place, COLUMN-MAJOR:
-// line kx holds the N values over y, so the heavy column pass streams whole
-// contiguous lines and the two transposes a 2-D FFT needs live in LDS tiles of
-// the row passes.
+// an optional single-pixel flip applied on the fly (env.py:164-172).  The
+// intermediates are COLUMN-MAJOR (a "line" kx holds the N values over y), so
+// the heavy column pass streams whole contiguous 8 KB lines and the two
+// transposes a 2-D FFT needs live in LDS tiles of the row passes:
 //
 //   k_rowfwd  GPB rows of a plane pair per block: bits -> one complex FFT per
 //             row pair (plane a real, plane b imaginary) -> Hermitian split ->
 //             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0) ->
-//             LDS tile transpose -> A[kx][y0..y0+GPB)        [HBM: read N^2/8 B, write 4 N^2 B per plane]
+//             LDS tile transpose -> A[kx][y0..y0+GPB)       [HBM: read N^2/8 B, write 4 N^2 B per plane]
 //   k_col     per half-spectrum line kx, two lane groups: FFT over y ->
-//             x H(kx, ky) -> IFFT -> line kx, and (Hermitian symmetry)
-//             conj F(kx, -ky) H(kx, ky) -> IFFT -> line N - kx (N/2 for
-//             kx = 0)                                                  [read 4 N^2, write 8 N^2]
+//             x H(kx, ky) -> IFFT -> B line kx, and (Hermitian symmetry)
+//             conj F(kx, -ky) H(kx, ky) -> IFFT -> B line N - kx (N/2 for
+//             kx = 0).  Lane groups loop over lines with the next input line
+//             prefetched into registers (no block barriers: A and B are
+//             separate buffers)                                  [read 4 N^2, write 8 N^2]
 //   k_rowinv  GPB rows per block, all P planes: LDS tile transpose of
-//             B[kx][y0..y0+GPB) -> IFFT over kx -> |U|^2 -> plane mean ->
-//             f64 partials of (I*T, I^2, T^2) against the target row  [read 8 N^2 per plane + 4 N^2]
+//             B[kx][y0..y0+GPB) (next plane's tile prefetched into registers
+//             behind LDS-only barriers) -> IFFT over kx -> |U|^2 -> plane
+//             mean -> f64 partials of (I*T, I^2, T^2) vs the target row   [read 8 N^2 per plane + 4 N^2]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -45,7 +47,7 @@ __device__ __forceinline__ int tile_pos(int line, int r) {
 template <int R>
 __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ jobs,
                                                    const uint32_t* __restrict__ mask,
-                                                   float2* __restrict__ ws,
+                                                   float2* __restrict__ ws_a,
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int CH, float va, float vb) {
   constexpr int N = R * R;
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ j
   }
   __syncthreads();  // tw visible
   fft_group<R, false>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
-  __syncthreads();  // every group is done with its scratch: reuse as the tile
+  lds_barrier();    // every group is done with its scratch: reuse as the tile
 
   // Hermitian split -> tile[plane][kx][row]
   float2* tile = lds;
@@ -128,44 +130,48 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ j
     tile[tile_pos<R>(kx, grp)] = fa;
     tile[tile_pos<R>(N / 2 + kx, grp)] = fb;
   }
-  __syncthreads();
+  lds_barrier();
   // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
-  float2* base = ws + ((size_t)j * P + pa) * N * N;
+  float2* base = ws_a + ((size_t)j * P + pa) * (N / 2) * N;
   constexpr int CHUNKS = N * GPB / 2;
   static_assert(CHUNKS % 256 == 0, "chunking");
 #pragma unroll
   for (int i = 0; i < CHUNKS / 256; ++i) {
     const int c = threadIdx.x + 256 * i;
     const int r2 = (c % (GPB / 2)) * 2;
-    const int line = c / (GPB / 2);  // pl * N/2 + kx
+    const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
     const float2 a = tile[tile_pos<R>(line, r2)];
     const float2 b = tile[tile_pos<R>(line, r2 + 1)];
-    const int pl = line / (N / 2), kx = line % (N / 2);
-    *reinterpret_cast<float4*>(base + (size_t)pl * N * N + (size_t)kx * N + y0 + r2) =
-        make_float4(a.x, a.y, b.x, b.y);
+    *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
   }
 }
 
 // ---------------------------------------------------------------------------
 // Pass 2
 // ---------------------------------------------------------------------------
-// Block = 8 lane groups = LPB lines x 2 roles (waves 0..W/2-1 role 1, the
-// rest role 2, so the role is uniform per wave).  Both roles FFT the same
-// input line (the second read hits L2); role 1 writes line kx, role 2 the
-// mirrored line.  One R-value array per lane: no spills at R = 32.
+// Block = 8 lane groups = LPB lines x 2 roles (the first half of the waves
+// role 1, the rest role 2, so the role is uniform per wave); each group walks
+// ITER lines.  Both roles FFT the same input line (the second read hits
+// L2); role 1 writes B line kx, role 2 the mirrored line:
 //   role 1: G = a1 H(kx),  a1 = Z            (kx != 0)   a1 = (Z + M)/2     (kx == 0)
 //   role 2: G = a2 H(kx),  a2 = M            (kx != 0)   a2 = -i (Z - M)/2, H(N/2, .)  (kx == 0)
 // with Z = F(kx, ky), M = conj F(kx, -ky) (H is even in fx: H(N-kx) = H(kx)).
 template <int R>
+__host__ __device__ constexpr int col_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
+
+template <int R>
 __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs,
-                                                float2* __restrict__ ws,
+                                                const float2* __restrict__ ws_a,
+                                                float2* __restrict__ ws_b,
                                                 const float2* __restrict__ htab,
                                                 const float2* __restrict__ tw_glob, int P) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // lane groups per block
-  constexpr int LPB = GPB / 2;          // lines per block
-  constexpr int LB = (N / 2) / LPB;
+  constexpr int LPB = GPB / 2;          // lines per block per iteration
+  constexpr int ITER = col_iters<R>();
+  constexpr int LB = (N / 2) / (LPB * ITER);
   static_assert(GPB % 2 == 0 && (64 / R) <= LPB, "role must be wave-uniform");
+  static_assert((N / 2) % (LPB * ITER) == 0, "line blocking");
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
 
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
-  const int role2 = grp >= LPB;
+  const bool role2 = grp >= LPB;
   int bid = blockIdx.x;
   const int lb = bid % LB;
   bid /= LB;
@@ -181,46 +187,57 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
   const int j = bid / P;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;
-  const int kx = lb * LPB + (grp % LPB);
-  float2* plane = ws + ((size_t)j * P + p) * N * N;
-  const float2* in = plane + (size_t)kx * N;
-
-  float2 v[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) v[jj] = in[t + R * jj];
-  // tw visible, and EVERY group's input loads have landed before any group
-  // stores: role 1 overwrites line kx, which role 2 reads (in-place pass)
-  __syncthreads();
+  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N;
+  float2* bout = ws_b + ((size_t)j * P + p) * N * N;
+  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N;
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
-  fft_group<R, false>(v, t, sc, tw);
+  const int kx0 = lb * (LPB * ITER) + (grp % LPB);
 
-  // F (natural order: lane t, register k2 -> ky = t + R k2) into the scratch,
-  // then M[k2] = conj F(-ky) read back from lane (R - t) mod R.
-  wave_sync();
+  float2 nxt[R];
 #pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
-  wave_sync();
-  const bool dc = (kx == 0);
-  // a = alpha Z + beta M (complex per-lane coefficients: branch-free)
-  float2 alpha, beta;
-  if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
-                beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
-  else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
-                beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
-  const float2* hp = htab + (size_t)jb.group * (N / 2 + 1) * N + (size_t)((role2 && dc) ? N / 2 : kx) * N;
-  const int tm = (R - t) & (R - 1);
+  for (int jj = 0; jj < R; ++jj) nxt[jj] = ain[(size_t)kx0 * N + t + R * jj];
+  lds_barrier();  // tw visible (the line loads stay in flight)
+
+#pragma unroll 1
+  for (int it = 0; it < ITER; ++it) {
+    const int kx = kx0 + it * LPB;
+    float2 v[R];
 #pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) {
-    // conj F(N - ky): lane tm, register R-1-k2 (lane 0: its own register (R-k2) mod R)
-    const float2 mm = (t == 0) ? *sc.at(0, (R - k2) & (R - 1)) : *sc.at(tm, R - 1 - k2);
-    const float2 m = conjf2(mm);
-    const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, m));
-    v[k2] = cmul(a, hp[t + R * k2]);
+    for (int jj = 0; jj < R; ++jj) v[jj] = nxt[jj];
+    if (it + 1 < ITER) {  // next line in flight under this line's FFTs
+      const float2* in = ain + (size_t)(kx + LPB) * N;
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) nxt[jj] = in[t + R * jj];
+    }
+    fft_group<R, false>(v, t, sc, tw);
+
+    // F (natural order: lane t, register k2 -> ky = t + R k2) into the scratch,
+    // then M[k2] = conj F(-ky) read back from lane (R - t) mod R.
+    wave_sync();
+#pragma unroll
+    for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
+    wave_sync();
+    const bool dc = (kx == 0);
+    // a = alpha Z + beta M with per-lane complex coefficients: branch-free
+    float2 alpha, beta;
+    if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
+                  beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
+    else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
+                  beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
+    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N;
+    const int tm = (R - t) & (R - 1);
+#pragma unroll
+    for (int k2 = 0; k2 < R; ++k2) {
+      // conj F(N - ky): lane tm, register R-1-k2 (lane 0: own register (R-k2) mod R)
+      const float2 mm = (t == 0) ? *sc.at(0, (R - k2) & (R - 1)) : *sc.at(tm, R - 1 - k2);
+      const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, conjf2(mm)));
+      v[k2] = cmul(a, hp[t + R * k2]);
+    }
+    fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
+    float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
+#pragma unroll
+    for (int k2 = 0; k2 < R; ++k2) out[t + R * k2] = v[k2];
   }
-  fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: M reads are done
-  float2* out = plane + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
-#pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) out[t + R * k2] = v[k2];
 }
 
 // ---------------------------------------------------------------------------
@@ -228,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 // ---------------------------------------------------------------------------
 template <int R>
 __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ jobs,
-                                                   const float2* __restrict__ ws,
+                                                   const float2* __restrict__ ws_b,
                                                    const float* __restrict__ target,
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int G, double* __restrict__ partial,
@@ -239,8 +256,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
   constexpr int CH16 = N * GPB / 2;     // 16-B chunks per plane tile
   constexpr int PER = CH16 / 256;
   static_assert(CH16 % 256 == 0, "chunking");
-  __shared__ float2 tw[N];
   constexpr int SCR = GPB * R * (R + 1);   // padded transpose scratch reuses the tile
+  __shared__ float2 tw[N];
   __shared__ __attribute__((aligned(16))) float2 tile[SCR > N * GPB ? SCR : N * GPB];
   __shared__ double red[GPB][3];
 
@@ -260,23 +277,22 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
   }
   const int y0 = rb * GPB;
   const int y = y0 + grp;
-  const float2* jbase = ws + (size_t)j * P * N * N;
+  const float2* jbase = ws_b + (size_t)j * P * N * N;
 
+  float4 pre[PER];   // this thread's share of a plane tile, one plane ahead
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
+    pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * N + y0 + r2);
+  }
   float acc[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) acc[k] = 0.0f;
 
 #pragma unroll 1
   for (int p = 0; p < P; ++p) {
-    const float2* pb = jbase + (size_t)p * N * N;
-    float4 pre[PER];   // all of this thread's tile loads in flight at once
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-      pre[i] = *reinterpret_cast<const float4*>(pb + (size_t)line * N + y0 + r2);
-    }
-    __syncthreads();  // previous plane's scratch use is over
+    lds_barrier();  // previous plane's scratch use is over (also publishes tw)
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = threadIdx.x + 256 * i;
@@ -284,14 +300,20 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
       tile[tile_pos<R>(line, r2)] = make_float2(pre[i].x, pre[i].y);
       tile[tile_pos<R>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
     }
-    __syncthreads();
+    if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
+      const float2* nb = jbase + (size_t)(p + 1) * N * N;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
+        pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * N + y0 + r2);
+      }
+    }
+    lds_barrier();
     float2 v[R];
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) {
-      const int kx = t + R * jj;
-      v[jj] = tile[tile_pos<R>(kx, grp)];
-    }
-    __syncthreads();  // tile consumed: reuse it as transpose scratch
+    for (int jj = 0; jj < R; ++jj) v[jj] = tile[tile_pos<R>(t + R * jj, grp)];
+    lds_barrier();  // tile consumed: reuse it as transpose scratch
     fft_group<R, true>(v, t, PaddedScratch<R>{tile + grp * R * (R + 1)}, tw);
 #pragma unroll
     for (int k = 0; k < R; ++k) acc[k] += norm2(v[k]);
@@ -349,20 +371,22 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / GPB);
     if (tm) tm->begin(0, st);
-    hipLaunchKernelGGL(k_rowfwd<R>, dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws, pd.tw, P,
+    hipLaunchKernelGGL(k_rowfwd<R>, dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);
     if (tm) tm->end(0, n_jobs, st);
   }
   {
-    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / (GPB / 2));
+    constexpr int LINES_PER_BLOCK = (GPB / 2) * col_iters<R>();
+    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
     if (tm) tm->begin(1, st);
-    hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws, pd.htab, pd.tw, P);
+    hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
+                       pd.tw, P);
     if (tm) tm->end(1, n_jobs, st);
   }
   {
     const unsigned blocks = (unsigned)n_jobs * (N / GPB);
     if (tm) tm->begin(2, st);
-    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws, target, pd.tw,
+    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target, pd.tw,
                        P, pd.G, pd.partial, inten_out);
     if (tm) tm->end(2, n_jobs, st);
   }
