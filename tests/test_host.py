@@ -1,0 +1,111 @@
+"""Host-side logic without a GPU: bit packing, spaces, DBS speculation
+bookkeeping, pre-model binning -- each checked against the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hbx_oracle as O
+
+
+def test_pack_bits_torch_matches_oracle():
+    from hbx.plan import pack_bits, unpack_bits
+    m = (np.random.default_rng(0).random((2, 3, 128)) > 0.5).astype(np.uint8)
+    got = pack_bits(torch.from_numpy(m)).numpy().view("<u8")
+    assert np.array_equal(got, O.pack_mask(m))
+    assert np.array_equal(unpack_bits(torch.from_numpy(got.view(np.int64)), 128).numpy(), m)
+
+
+def test_pack_bits_bit63():
+    from hbx.plan import pack_bits
+    m = torch.zeros(1, 64, dtype=torch.uint8)
+    m[0, 63] = 1
+    assert pack_bits(m).numpy().view("<u8")[0] == np.uint64(1 << 63)
+
+
+def test_pack_bits_rejects_ragged_width():
+    from hbx.plan import pack_bits
+    with pytest.raises(ValueError):
+        pack_bits(torch.zeros(4, 100))
+
+
+def test_spaces_surface():
+    from hbx import spaces
+    d = spaces.Discrete(8 * 256 * 256)
+    assert d.n == 524288 and d.contains(524287) and not d.contains(524288)
+    b = spaces.Box(0, 1, (1, 8, 4, 4), np.int8)
+    assert b.sample().shape == (1, 8, 4, 4)
+    md = spaces.MultiDiscrete([8, 256, 256])
+    s = md.sample()
+    assert md.contains(s)
+
+
+def test_first_improving_is_strict():
+    from hbx.dbs import first_improving
+    assert first_improving(np.array([1.0, 2.0, 2.5]), 2.0) == 2
+    assert first_improving(np.array([1.0, 2.0]), 2.0) is None
+    assert first_improving(np.array([3.0]), 2.0) == 0
+
+
+def test_speculative_walk_equals_serial():
+    """The speculative batching rule reproduces the serial accept sequence on any
+    deterministic evaluator (here a toy 'psnr' = running sum of per-index gains)."""
+    from hbx.dbs import KController, first_improving
+    rng = np.random.default_rng(1)
+    gains = rng.normal(size=2000)
+    # serial
+    prev, acc_serial = 0.0, []
+    for i, g in enumerate(gains):
+        if prev + g > prev:
+            prev += g
+            acc_serial.append(i)
+    # speculative, evaluating candidates against the base
+    prev, acc, pos, ctl = 0.0, [], 0, KController(k_min=2, k_max=64, k0=8)
+    while pos < len(gains):
+        k = min(ctl.k, len(gains) - pos)
+        ps = prev + gains[pos:pos + k]
+        i = first_improving(ps, prev)
+        ctl.update(i)
+        if i is None:
+            pos += k
+            continue
+        prev = ps[i]
+        acc.append(pos + i)
+        pos += i + 1
+    assert acc == acc_serial
+
+
+def test_premodel_bins_match_oracle():
+    from hbx.dbs import premodel_bins
+    vals = np.concatenate([np.linspace(-0.1, 1.1, 241), np.round(np.linspace(0, 1, 11), 10)])
+    got = premodel_bins(vals)
+    want = np.array([O.premodel_bin(float(v)) for v in vals])
+    assert np.array_equal(got, want)
+
+
+def test_shard_range_covers_everything():
+    from hbx.dist import shard_range
+    for total in (0, 1, 7, 128, 1024, 1025):
+        for world in (1, 2, 3, 8):
+            parts = [shard_range(total, r, world) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == total
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_optics_config_to_c():
+    from hbx.plan import rgb_config
+    c = rgb_config(1024).to_c()
+    assert (c.height, c.groups, c.planes) == (1024, 3, 8)
+    assert abs(c.wavelength[2] - 450e-9) < 1e-18 and c.z == 2e-3
+    with pytest.raises(ValueError):
+        from hbx.plan import OpticsConfig
+        OpticsConfig(64, 64, 2, 2, (515e-9,)).to_c()
+
+
+def test_plan_requires_gpu():
+    import hbx
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        hbx.Plan(hbx.mono_config(64))
