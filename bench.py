@@ -9,6 +9,11 @@ flip -> re-propagate the touched colour group (8 planes, 2-D FFT ASM) ->
 (env.py:154-259; DBS_1024_24.py:313-422).  Synthetic data:
 pre_model ~ U[0,1) -> mask = pre >= 0.5, target ~ U[0,1), actions ~ U{0..CH*N^2-1}.
 
+The headline `value` is the FFT mode (the reference's algorithm: the whole
+touched colour group is re-propagated every step).  The incremental-field
+mode (SURVEY 8d "reported separately") is measured afterwards on the same
+workload and reported under `incremental_psf_mode`.
+
 N GPUs: one process per GPU (torchrun), 128 envs per rank (weak scaling), the
 per-step rewards / psnr / done flags gathered to rank 0 over RCCL.
 
@@ -41,19 +46,25 @@ def parse():
                     help="env-steps of the numpy oracle timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-psnr-check", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-psf", action="store_true", help="skip the incremental-mode measurement")
+    ap.add_argument("--psf-steps", type=int, default=200)
     ap.add_argument("--chunk", type=int, default=0,
                     help="jobs per launch sequence (0 = all envs at once)")
     return ap.parse_args()
 
 
 def algorithmic_bytes(N: int, P: int):
-    """HBM bytes each pass must move per job (one colour group of one env):
+    """HBM bytes each kernel must move per job (one colour group of one env):
     k_rowfwd: read P*N^2/8 mask bits, write P*N^2/2 complex64 (half spectrum)
     k_col:    read P*N^2/2 complex64, write P*N^2 complex64
-    k_rowinv: read P*N^2 complex64 + N^2 f32 target."""
+    k_rowinv: read P*N^2 complex64 + N^2 f32 target
+    k_psf_eval:   read the touched plane's field (8 N^2) + group intensity (4 N^2) + target (4 N^2)
+    k_psf_commit: accepted envs only: read + write field and intensity (24 N^2)."""
     return {"k_rowfwd": P * N * N // 8 + P * N * N * 4,
             "k_col": P * N * N * 4 + P * N * N * 8,
-            "k_rowinv": P * N * N * 8 + N * N * 4}
+            "k_rowinv": P * N * N * 8 + N * N * 4,
+            "k_psf_eval": 16 * N * N,
+            "k_psf_commit": 24 * N * N}
 
 
 def cpu_baseline(n_steps: int, N: int):
@@ -104,22 +115,39 @@ def load_pmc_traffic():
         return None
 
 
+def pass_table(timing, abytes):
+    passes = {}
+    for name, (ms, launches, jobs) in timing.items():
+        if launches:
+            avg = ms / launches
+            per_launch = abytes[name] * (jobs / launches)
+            passes[name] = {"avg_ms": avg, "launches": launches, "jobs_per_launch": jobs / launches,
+                            "alg_bytes_per_launch": per_launch,
+                            "achieved_GBs": per_launch / (avg * 1e-3) / 1e9}
+    return passes
+
+
+def rounded(passes):
+    return {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+            for k, v in passes.items()}
+
+
 def main():
     args = parse()
-    import numpy as np
     import torch
     from hbx import dist as hd
     from hbx.env import HologramVecEnv
     from hbx.plan import rgb_config
 
     rank, world, local = hd.init()
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     N, B = args.size, args.envs
     cfg = rgb_config(N)
     CH, G, P = cfg.channels, cfg.groups, cfg.planes
+    gather = (world > 1) and not args.no_gather
 
     # synthetic, seeded per global env index
     def target_source(i):
@@ -130,91 +158,107 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i))
         return torch.rand((CH, N, N), generator=g, device="cuda")
 
-    vec = HologramVecEnv(cfg, B, target_source, pre_model_source=pre_model_source, obs_keys=(),
-                         auto_reset=False, max_steps=10 ** 9, max_jobs=args.chunk or None)
-    vec.reset()
-    gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
-    n_act = CH * N * N
-    total_steps = args.warmup + args.steps
-    actions = torch.randint(0, n_act, (total_steps, B), generator=gen, device="cuda", dtype=torch.int64)
-    gather = (world > 1) and not args.no_gather
+    def measure(mode: str, steps: int, warmup: int):
+        vec = HologramVecEnv(cfg, B, target_source, pre_model_source=pre_model_source, obs_keys=(),
+                             auto_reset=False, max_steps=10 ** 9, max_jobs=args.chunk or None, mode=mode,
+                             refresh_every=0)
+        vec.reset()
+        gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
+        total = warmup + steps
+        actions = torch.randint(0, CH * N * N, (total, B), generator=gen, device="cuda", dtype=torch.int64)
 
-    def one_step(k):
-        r, ps, acc, term, trunc = vec.step_device(actions[k])
-        if gather:
-            hd.gather_to_rank0(hd.pack_step_metrics(r, ps, acc, term, trunc))
+        def one_step(k):
+            r, ps, acc, term, trunc = vec.step_device(actions[k])
+            if gather:
+                hd.gather_to_rank0(hd.pack_step_metrics(r, ps, acc, term, trunc))
 
-    for k in range(args.warmup):
-        one_step(k)
-    torch.cuda.synchronize()
-    per_step_launches = -(-B // (args.chunk or B))
-    vec.plan.set_timing(args.steps * per_step_launches + 1)
-    hd.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.warmup, total_steps):
-        one_step(k)
-    torch.cuda.synchronize()
-    hd.barrier()
-    dt_local = time.perf_counter() - t0
-    dt = hd.max_over_ranks(dt_local, torch.device("cuda", local))
-    timing = vec.plan.read_timing()
-    vec.state.check_error()
+        for k in range(warmup):
+            one_step(k)
+        torch.cuda.synchronize()
+        vec.plan.set_timing(steps * -(-B // (args.chunk or B)) + 1)
+        hd.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(warmup, total):
+            one_step(k)
+        torch.cuda.synchronize()
+        hd.barrier()
+        dt = hd.max_over_ranks(time.perf_counter() - t0, dev)
+        timing = vec.plan.read_timing()
+        vec.state.check_error()
+        acc_rate = float(vec.state.flip_count.sum().item()) / float(vec.state.steps.sum().item())
+        return vec, dt, timing, acc_rate
 
-    env_steps = B * world * args.steps
-    value = env_steps / dt
+    vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup)
+    value = B * world * args.steps / dt
     ms_per_step = dt / args.steps * 1e3
-
-    if rank != 0:
-        return
     abytes = algorithmic_bytes(N, P)
-    passes = {}
-    for name, (ms, launches, jobs) in timing.items():
-        if launches:
-            avg = ms / launches
-            per_launch = abytes[name] * (jobs / launches)
-            passes[name] = {"avg_ms": avg, "launches": launches, "jobs_per_launch": jobs / launches,
-                            "alg_bytes_per_launch": per_launch,
-                            "achieved_GBs": per_launch / (avg * 1e-3) / 1e9}
-    dom = max(passes, key=lambda n: passes[n]["avg_ms"])
-    d = passes[dom]
-    pmc = load_pmc_traffic()
-    traffic = None
-    if pmc and dom in pmc.get("kernels", {}):
-        kinfo = pmc["kernels"][dom]
-        if kinfo.get("jobs_per_launch") == d["jobs_per_launch"] and kinfo.get("N") == N:
-            traffic = kinfo.get("hbm_bytes_per_launch")
-    roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
-    step_bytes = sum(abytes.values()) * B
-    out = {
-        "metric": "env-steps/sec (1024x1024, 24-plane)",
-        "value": round(value, 2),
-        "unit": "env-steps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (seeded U[0,1) pre-model/targets, uniform actions)",
-        "config": {"workload": "configs[2]: batched VecEnv.step, 128 envs/GPU x 1024x1024x24-plane "
-                               "(3 colour groups x 8 planes), one action per env per step",
-                   "envs_per_gpu": B, "global_envs": B * world, "size": N, "planes": CH,
-                   "parallelism": f"env-sharded x{world}" + (" + RCCL metric gather" if gather else "")},
-        "roofline": roofline,
-        "passes": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                   for k, v in passes.items()},
-        "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-    }
-    if world == 1 and not args.no_psnr_check:
-        out["psnr_delta_vs_numpy"] = psnr_check(vec, N)
-    if world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, N)
-    print(json.dumps(out), flush=True)
+    passes = pass_table(timing, abytes)
+    out = None
+    if rank == 0:
+        dom = max(passes, key=lambda n: passes[n]["avg_ms"])
+        d = passes[dom]
+        pmc = load_pmc_traffic()
+        traffic = None
+        if pmc and dom in pmc.get("kernels", {}):
+            kinfo = pmc["kernels"][dom]
+            if kinfo.get("jobs_per_launch") == d["jobs_per_launch"] and kinfo.get("N") == N:
+                traffic = kinfo.get("hbm_bytes_per_launch")
+        roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
+        step_bytes = (abytes["k_rowfwd"] + abytes["k_col"] + abytes["k_rowinv"]) * B
+        out = {
+            "metric": "env-steps/sec (1024x1024, 24-plane)",
+            "value": round(value, 2),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded U[0,1) pre-model/targets, uniform actions)",
+            "config": {"workload": "configs[2]: batched VecEnv.step, 128 envs/GPU x 1024x1024x24-plane "
+                                   "(3 colour groups x 8 planes), one action per env per step, FFT mode "
+                                   "(whole touched group re-propagated)",
+                       "envs_per_gpu": B, "global_envs": B * world, "size": N, "planes": CH,
+                       "parallelism": f"env-sharded x{world}" + (" + RCCL metric gather" if gather else "")},
+            "roofline": roofline,
+            "passes": rounded(passes),
+            "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            "accept_rate": round(acc_rate, 4),
+        }
+        if world == 1 and not args.no_psnr_check:
+            out["psnr_delta_vs_numpy"] = psnr_check(vec, N)
+    vec.close()
+    del vec
+    torch.cuda.empty_cache()
+
+    if not args.no_psf:
+        vec, dt, timing, acc_rate = measure("psf", args.psf_steps, max(args.warmup, 5))
+        if rank == 0:
+            ps = pass_table(timing, abytes)
+            ev = ps.get("k_psf_eval")
+            out["incremental_psf_mode"] = {
+                "value": round(B * world * args.psf_steps / dt, 2), "unit": "env-steps/s",
+                "steps": args.psf_steps, "ms_per_step": round(dt / args.psf_steps * 1e3, 4),
+                "accept_rate": round(acc_rate, 4),
+                "roofline": None if ev is None else {
+                    "bound": "hbm", "kernel": "k_psf_eval", "achieved": round(ev["achieved_GBs"], 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ev["achieved_GBs"] / HBM_PEAK_GBS, 4),
+                    "kernel_avg_ms": round(ev["avg_ms"], 4)},
+                "passes": rounded(ps),
+                "note": "same env semantics; a flip adds +-h_g(shifted) to the touched plane's cached field "
+                        "(linearity of the propagation), no FFT per step; reported separately per SURVEY 8d"}
+        vec.close()
+
+    if rank == 0:
+        if world == 1 and args.cpu_sample > 0:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_sample, N)
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -158,6 +158,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "accept_flag");
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
+  if (hipMalloc(&pd.psf_partial, (size_t)max_jobs * hbx::kPsfBlocks * 2 * sizeof(double)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "psf partials");
   if (hipMemcpy(pd.tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess)
@@ -179,6 +181,8 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->job_inten) (void)hipFree(p->job_inten);
   if (p->accept_flag) (void)hipFree(p->accept_flag);
   if (p->err) (void)hipFree(p->err);
+  if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
+  if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
   hbx_plan_set_timing(p, 0);
   delete p;
   return HBX_OK;
@@ -199,6 +203,60 @@ int ensure_job_inten(hbx_plan_t p) {
 
 double pixel_count(const hbx_plan_t p) {
   return (double)p->pd.G * (double)p->pd.N * (double)p->pd.N;
+}
+
+// Single-pixel fields h_g = IFFT2(H_g), computed once with the exact FFT path:
+// one env whose mask has only pixel (0, 0) of plane g*P set, propagated as an
+// amplitude field (va = 0, vb = 1) whatever the plan's field encoding, so
+// plane g*P's output field is h_g.  Allocates: call outside graph capture.
+int ensure_hpsf(hbx_plan_t p, hipStream_t st) {
+  PlanDev& pd = p->pd;
+  if (pd.hpsf) return HBX_OK;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  const size_t hw = (size_t)N * N;
+  uint64_t* mask = nullptr;
+  float* target = nullptr;
+  float2* field = nullptr;
+  float2* h = nullptr;
+  auto release = [&]() {
+    if (mask) (void)hipFree(mask);
+    if (target) (void)hipFree(target);
+    if (field) (void)hipFree(field);
+  };
+  if (hipMalloc(&mask, (size_t)CH * N * (N / 64) * sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&target, (size_t)G * hw * sizeof(float)) != hipSuccess ||
+      hipMalloc(&field, (size_t)CH * hw * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&h, (size_t)G * hw * sizeof(float2)) != hipSuccess) {
+    release();
+    if (h) (void)hipFree(h);
+    return fail(HBX_ERR_NOMEM, "single-pixel field tables");
+  }
+  std::vector<uint64_t> m((size_t)CH * N * (N / 64), 0);
+  for (int g = 0; g < G; ++g) m[(size_t)g * P * N * (N / 64)] = 1ull;  // pixel (0,0) of plane g*P
+  if (hipMemcpyAsync(mask, m.data(), m.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st) != hipSuccess ||
+      hipMemsetAsync(target, 0, (size_t)G * hw * sizeof(float), st) != hipSuccess) {
+    release();
+    (void)hipFree(h);
+    return fail(HBX_ERR_HIP, "single-pixel field setup");
+  }
+  PlanDev amp = pd;
+  amp.va = 0.0f;
+  amp.vb = 1.0f;
+  amp.timer = nullptr;
+  hipError_t e = hbx::launch_jobs_full(nullptr, 1, G, p->jobs, st);
+  if (e == hipSuccess)
+    e = hbx::run_jobs(amp, p->jobs, G, reinterpret_cast<const uint32_t*>(mask), target, nullptr, field, st);
+  for (int g = 0; g < G && e == hipSuccess; ++g)
+    e = hipMemcpyAsync(h + (size_t)g * hw, field + (size_t)g * P * hw, hw * sizeof(float2),
+                       hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  release();
+  if (e != hipSuccess) {
+    (void)hipFree(h);
+    return fail(HBX_ERR_HIP, std::string("single-pixel field: ") + hipGetErrorString(e));
+  }
+  pd.hpsf = h;
+  return HBX_OK;
 }
 
 EnvDev env_dev(const hbx_env_buffers_t* e) {
@@ -228,7 +286,7 @@ EnvDev env_offset(const EnvDev& d, size_t e0, int CH, int G, int N) {
 // full propagation of n_ids envs (absolute ids from env_ids, or 0..n_ids-1)
 int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, const int32_t* env_ids,
                    int n_ids, float* intensity, double* chan_stats, double* psnr, const EnvDev* env,
-                   hipStream_t st) {
+                   float2* field, hipStream_t st) {
   const PlanDev& pd = p->pd;
   const int G = pd.G;
   const int chunk = p->max_jobs / G;
@@ -246,8 +304,9 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
     const size_t mwords = (size_t)G * pd.P * pd.N * (pd.N / 64);
     const uint64_t* m = env_ids ? mask : mask + (size_t)i0 * mwords;
     const float* tg = env_ids ? target : target + (size_t)i0 * G * pd.N * pd.N;
+    float2* fo = field ? (env_ids ? field : field + (size_t)i0 * G * pd.P * pd.N * pd.N) : nullptr;
     HBX_HIP(hbx::run_jobs(pd, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
-                          intensity ? p->job_inten : nullptr, st));
+                          intensity ? p->job_inten : nullptr, fo, st));
     double* cs = env_ids ? chan_stats : chan_stats + (size_t)i0 * G * 3;
     double* ps = psnr ? (env_ids ? psnr : psnr + i0) : nullptr;
     EnvDev ed = dummy;
@@ -275,7 +334,7 @@ int hbx_propagate(hbx_plan_t p, const uint64_t* mask, const float* target, int32
   if (n_env == 0) return HBX_OK;
   HBX_HIP(hipSetDevice(p->device));
   return propagate_full(p, mask, target, nullptr, n_env, intensity, chan_stats, psnr, nullptr,
-                        (hipStream_t)stream);
+                        nullptr, (hipStream_t)stream);
 }
 
 int hbx_psnr(hbx_plan_t p, const double* chan_stats, int32_t n_env, double* psnr, void* stream) {
@@ -305,8 +364,71 @@ int hbx_env_reset(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const
   const int CH = pd.G * pd.P;
   if (e->record)
     HBX_HIP(hbx::launch_zero_record(e->record, env_ids, n, (size_t)CH * pd.N * pd.N, st));
+  if (e->field) {
+    if (!e->intensity) return fail(HBX_ERR_INVALID, "env.field needs env.intensity");
+    rc = ensure_hpsf(p, st);
+    if (rc) return rc;
+  }
   EnvDev ed = env_dev(e);
-  return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed, st);
+  return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed,
+                        reinterpret_cast<float2*>(e->field), st);
+}
+
+int hbx_field_refresh(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const int32_t* env_ids,
+                      int32_t n_ids, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!e || !e->mask || !e->target || !e->chan_stats || !e->intensity || !e->field)
+    return fail(HBX_ERR_INVALID, "refresh needs mask, target, chan_stats, intensity and field");
+  const int n = env_ids ? n_ids : n_env;
+  if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  rc = ensure_hpsf(p, st);
+  if (rc) return rc;
+  return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, nullptr,
+                        reinterpret_cast<float2*>(e->field), st);
+}
+
+int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_t* prm,
+                     int32_t n_env, const int64_t* actions, double* reward, double* psnr,
+                     uint8_t* accepted, uint8_t* terminated, uint8_t* truncated, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!e || !prm || !actions || !e->mask || !e->target || !e->chan_stats || !e->init_psnr ||
+      !e->prev_psnr || !e->max_psnr_diff || !e->steps || !e->flip_count || !e->sustained ||
+      !e->intensity || !e->field)
+    return fail(HBX_ERR_INVALID, "env buffers incomplete (incremental mode needs field + intensity)");
+  if (!p->pd.hpsf) return fail(HBX_ERR_INVALID, "incremental mode: call hbx_env_reset with env.field first");
+  if (prm->accept_rule != HBX_ACCEPT_ENV && prm->accept_rule != HBX_ACCEPT_DBS)
+    return fail(HBX_ERR_INVALID, "accept_rule");
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  const size_t hw = (size_t)N * N;
+  EnvParams ep;
+  ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
+  ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
+  ep.accept_rule = prm->accept_rule;
+  const EnvDev base = env_dev(e);
+  for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, n_env - b0);
+    const EnvDev ed = env_offset(base, b0, CH, G, N);
+    float2* fld = reinterpret_cast<float2*>(e->field) + (size_t)b0 * CH * hw;
+    float* inten = e->intensity + (size_t)b0 * G * hw;
+    HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
+    HBX_HIP(hbx::launch_psf_eval(pd, p->jobs, n, ed.mask, fld, inten, ed.target, ed.chan_stats, st));
+    HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),
+                                          p->optics.rel_scale, p->optics.peak,
+                                          reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
+                                          accepted ? accepted + b0 : nullptr,
+                                          terminated ? terminated + b0 : nullptr,
+                                          truncated ? truncated + b0 : nullptr, p->accept_flag, st));
+    HBX_HIP(hbx::launch_psf_commit(pd, p->jobs, n, ed.mask, fld, inten, p->accept_flag, st));
+  }
+  return HBX_OK;
 }
 
 int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_t* prm,
@@ -341,7 +463,7 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     const EnvDev ed = env_offset(base, b0, CH, G, N);
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
     HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,
-                          want_inten ? p->job_inten : nullptr, st));
+                          want_inten ? p->job_inten : nullptr, nullptr, st));
     HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),
                                           p->optics.rel_scale, p->optics.peak,
                                           reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
@@ -375,7 +497,7 @@ int hbx_step(hbx_plan_t p, uint64_t* mask, const int64_t* actions, int32_t n_env
     uint64_t* m = mask + (size_t)b0 * CH * N * (N / 64);
     const float* tg = target + (size_t)b0 * G * N * N;
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, p->err, st));
-    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(m), tg, nullptr, st));
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(m), tg, nullptr, nullptr, st));
     HBX_HIP(hbx::launch_dbs_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, m,
                                           chan_stats + (size_t)b0 * G * 3, prev_psnr + b0,
                                           psnr_out ? psnr_out + b0 : nullptr,
@@ -400,7 +522,8 @@ int hbx_eval_flips(hbx_plan_t p, const uint64_t* base_mask, const float* target,
   for (int k0 = 0; k0 < K; k0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, K - k0);
     HBX_HIP(hbx::launch_jobs_from_flips(flips + k0, n, N, N, P, CH, p->jobs, st));
-    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr, st));
+    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,
+                          nullptr, st));
     HBX_HIP(hbx::launch_eval_finalize(p->jobs, pd.job_stats, n, G, base_chan_stats, psnr_out + k0,
                                       group_stats ? group_stats + (size_t)k0 * 3 : nullptr,
                                       pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
@@ -433,7 +556,7 @@ int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
   (void)hipSetDevice(p->device);
   hbx::PassTimer* tm = p->pd.timer;
   if (tm) {
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < hbx::kNumPasses; ++k) {
       for (int i = 0; i < 2 * tm->capacity; ++i) (void)hipEventDestroy(tm->ev[k][i]);
       delete[] tm->ev[k];
     }
@@ -444,7 +567,7 @@ int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
   tm = new (std::nothrow) hbx::PassTimer();
   if (!tm) return fail(HBX_ERR_NOMEM, "timer");
   tm->capacity = capacity;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < hbx::kNumPasses; ++k) {
     tm->ev[k] = new (std::nothrow) hipEvent_t[2 * (size_t)capacity];
     if (!tm->ev[k]) return fail(HBX_ERR_NOMEM, "timer events");
     for (int i = 0; i < 2 * capacity; ++i) HBX_HIP(hipEventCreate(&tm->ev[k][i]));
@@ -458,14 +581,14 @@ int hbx_plan_read_timing(hbx_plan_t p, double* ms_total, int64_t* launches, int6
   if (rc) return rc;
   if (!ms_total || !launches) return fail(HBX_ERR_INVALID, "null output");
   hbx::PassTimer* tm = p->pd.timer;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < hbx::kNumPasses; ++k) {
     ms_total[k] = 0.0;
     launches[k] = 0;
     if (jobs) jobs[k] = 0;
   }
   if (!tm) return fail(HBX_ERR_INVALID, "timing not enabled");
   (void)hipSetDevice(p->device);
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < hbx::kNumPasses; ++k) {
     double tot = 0.0;
     for (int i = 0; i < tm->count[k]; ++i) {
       HBX_HIP(hipEventSynchronize(tm->ev[k][2 * i + 1]));

@@ -15,11 +15,12 @@ struct JobDesc {
 };
 
 // Optional hipEvent pairs around every pass launch (hbx_plan_set_timing).
+constexpr int kNumPasses = 5;  // rowfwd, col, rowinv, psf_eval, psf_commit
 struct PassTimer {
   int capacity = 0;
-  int count[3] = {0, 0, 0};
-  int64_t jobs[3] = {0, 0, 0};
-  hipEvent_t* ev[3] = {nullptr, nullptr, nullptr};  // [2 * capacity] start/stop
+  int count[kNumPasses] = {};
+  int64_t jobs[kNumPasses] = {};
+  hipEvent_t* ev[kNumPasses] = {};  // [2 * capacity] start/stop
   __host__ void begin(int pass, hipStream_t st) {
     if (capacity && count[pass] < capacity) (void)hipEventRecord(ev[pass][2 * count[pass]], st);
   }
@@ -42,8 +43,12 @@ struct PlanDev {
   float2* ws_b;        // [max_jobs][P][N][N]    after k_col (line kx, over y)
   double* partial;     // [max_jobs][N / (256/R)][3]
   double* job_stats;   // [max_jobs][3]
+  float2* hpsf;        // [G][N][N] single-pixel field h_g = IFFT2(H_g) (lazy, incremental mode)
+  double* psf_partial; // [max_jobs][kPsfBlocks][2]
   PassTimer* timer;    // nullable
 };
+
+constexpr int kPsfBlocks = 64;   // blocks per job of the incremental-field kernels
 
 struct EnvDev {
   uint64_t* mask;
@@ -67,8 +72,14 @@ struct EnvParams {
   int32_t accept_rule;
 };
 
+// field_out (nullable): [env][G*P][N][N] complex field of every propagated plane
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
-                    const float* target, float* inten_out, hipStream_t st);
+                    const float* target, float* inten_out, float2* field_out, hipStream_t st);
+hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
+                           const float2* field, const float* inten, const float* target,
+                           const double* chan_stats, hipStream_t st);
+hipError_t launch_psf_commit(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
+                             float2* field, float* inten, const int32_t* accept_flag, hipStream_t st);
 hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W, int P, int CH,
                                     JobDesc* jobs, int32_t* err, hipStream_t st);
 hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int P, int CH,

@@ -249,7 +249,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
                                                    const float* __restrict__ target,
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int G, double* __restrict__ partial,
-                                                   float* __restrict__ inten_out) {
+                                                   float* __restrict__ inten_out,
+                                                   float2* __restrict__ field_out) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // rows per block
   constexpr int RB = N / GPB;
@@ -317,6 +318,11 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
     fft_group<R, true>(v, t, PaddedScratch<R>{tile + grp * R * (R + 1)}, tw);
 #pragma unroll
     for (int k = 0; k < R; ++k) acc[k] += norm2(v[k]);
+    if (field_out) {  // exact field of this plane (incremental mode init / refresh)
+      float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * N + y) * N;
+#pragma unroll
+      for (int k = 0; k < R; ++k) frow[t + R * k] = v[k];
+    }
   }
 
   const float invp = 1.0f / (float)P;
@@ -362,7 +368,7 @@ __global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs
 template <int R>
 static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jobs,
                                 const uint32_t* mask, const float* target, float* inten_out,
-                                hipStream_t st) {
+                                float2* field_out, hipStream_t st) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;
   const int P = pd.P;
@@ -387,7 +393,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     const unsigned blocks = (unsigned)n_jobs * (N / GPB);
     if (tm) tm->begin(2, st);
     hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target, pd.tw,
-                       P, pd.G, pd.partial, inten_out);
+                       P, pd.G, pd.partial, inten_out, field_out);
     if (tm) tm->end(2, n_jobs, st);
   }
   hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial,
@@ -396,11 +402,11 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
 }
 
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
-                    const float* target, float* inten_out, hipStream_t st) {
+                    const float* target, float* inten_out, float2* field_out, hipStream_t st) {
   switch (pd.R) {
-    case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, st);
-    case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, st);
-    case 8: return launch_passes<8>(pd, jobs, n_jobs, mask, target, inten_out, st);
+    case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
+    case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
+    case 8: return launch_passes<8>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -1,0 +1,188 @@
+// hbx_psf.hip -- incremental-field ("PSF") mode kernels (gfx950).
+//
+// tt.simulate is linear in the field, so flipping pixel (c, r, col) of a mask
+// whose plane-c field U_c is known changes only that plane:
+//   U_c'(y, x) = U_c(y, x) + delta * h_g((y - r) mod N, (x - col) mod N)
+//   I_g'(y, x) = I_g(y, x) + (|U_c'|^2 - |U_c|^2) / P
+// with h_g = IFFT2(H_g) the field of a single unit pixel (computed once by
+// the exact FFT path) and delta = vb * (1 - 2 bit_old) the change of the
+// field value (amplitude: +-1, phase: -+2).  A step therefore streams U_c
+// (8 B/px), I_g (4 B/px) and the target channel (4 B/px) once -- no FFT --
+// and the relative-PSNR sums come out of the same pass.  h_g (8 B/px) is
+// shared by every env of the group and stays in L2 / the Infinity Cache.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbx_internal.hpp"
+
+namespace hbx {
+
+namespace {
+
+__device__ __forceinline__ float flip_delta(const uint64_t* mask, const JobDesc& jb, int N, int P,
+                                            int CH, float vb, bool after_flip) {
+  const int c = jb.group * P + jb.flip_plane;
+  const int r = jb.flip_pix / N, col = jb.flip_pix % N;
+  const uint64_t w = mask[(((size_t)jb.env * CH + c) * N + r) * (N / 64) + col / 64];
+  const int bit = (int)((w >> (col & 63)) & 1ull);
+  // before the flip: delta = vb (1 - 2 bit_old); after it: bit_new = 1 - bit_old
+  return after_flip ? vb * (float)(2 * bit - 1) : vb * (float)(1 - 2 * bit);
+}
+
+template <int BLK>
+__device__ __forceinline__ void block_sum2(double& a, double& b, double (*red)[2]) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    a += __shfl_xor(a, off, 64);
+    b += __shfl_xor(b, off, 64);
+  }
+  const int w = threadIdx.x / 64;
+  if ((threadIdx.x & 63) == 0) { red[w][0] = a; red[w][1] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a = 0.0; b = 0.0;
+    for (int i = 0; i < BLK / 64; ++i) { a += red[i][0]; b += red[i][1]; }
+  }
+}
+
+}  // namespace
+
+// grid (kPsfBlocks, n_jobs); each thread walks quads of 4 consecutive pixels
+__global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jobs,
+                                                  const uint64_t* __restrict__ mask,
+                                                  const float2* __restrict__ field,
+                                                  const float* __restrict__ inten,
+                                                  const float* __restrict__ target,
+                                                  const float2* __restrict__ hpsf, int N, int P,
+                                                  int G, float vb, double* __restrict__ partial) {
+  __shared__ double red[4][2];
+  const int j = blockIdx.y;
+  const JobDesc jb = jobs[j];
+  double sxy = 0.0, sxx = 0.0;
+  if (jb.env >= 0) {
+    const int CH = G * P;
+    const int g = jb.group;
+    const int r = jb.flip_pix / N, col = jb.flip_pix % N;
+    const float delta = flip_delta(mask, jb, N, P, CH, vb, false);
+    const float invp = 1.0f / (float)P;
+    const size_t hw = (size_t)N * N;
+    const float4* U = reinterpret_cast<const float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
+    const float4* I = reinterpret_cast<const float4*>(inten + ((size_t)jb.env * G + g) * hw);
+    const float4* T = reinterpret_cast<const float4*>(target + ((size_t)jb.env * G + g) * hw);
+    const float2* h = hpsf + (size_t)g * hw;
+    const int nq = (int)(hw / 4);
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
+      const int y = (4 * q) / N, x0 = (4 * q) % N;
+      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+      const float4 iv = I[q], tv = T[q];
+      const float2* hrow = h + (size_t)((y - r) & (N - 1)) * N;
+      const float2 h0 = hrow[(x0 - col) & (N - 1)], h1 = hrow[(x0 + 1 - col) & (N - 1)];
+      const float2 h2 = hrow[(x0 + 2 - col) & (N - 1)], h3 = hrow[(x0 + 3 - col) & (N - 1)];
+      const float uu[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
+      const float hh[8] = {h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
+      const float ii[4] = {iv.x, iv.y, iv.z, iv.w};
+      const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float ur = uu[2 * k], ui = uu[2 * k + 1];
+        const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
+        const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
+        const float In = fmaf(d, invp, ii[k]);
+        sxy = fma((double)In, (double)tt[k], sxy);
+        sxx = fma((double)In, (double)In, sxx);
+      }
+    }
+  }
+  block_sum2<256>(sxy, sxx, red);
+  if (threadIdx.x == 0) {
+    double* o = partial + ((size_t)j * kPsfBlocks + blockIdx.x) * 2;
+    o[0] = sxy; o[1] = sxx;
+  }
+}
+
+// fixed-order reduction of the block partials; sum T^2 of the touched channel
+// is unchanged by a flip and comes from the cached channel statistics
+__global__ void k_psf_reduce(const JobDesc* __restrict__ jobs, const double* __restrict__ partial,
+                             int n_jobs, int G, const double* __restrict__ chan_stats,
+                             double* __restrict__ job_stats) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_jobs) return;
+  const JobDesc jb = jobs[j];
+  double a = 0.0, b = 0.0;
+  const double* p = partial + (size_t)j * kPsfBlocks * 2;
+  for (int i = 0; i < kPsfBlocks; ++i) { a += p[2 * i]; b += p[2 * i + 1]; }
+  job_stats[3 * j] = a;
+  job_stats[3 * j + 1] = b;
+  job_stats[3 * j + 2] = jb.env >= 0 ? chan_stats[((size_t)jb.env * G + jb.group) * 3 + 2] : 0.0;
+}
+
+// accepted envs: rewrite U_c and I_g (the mask bit is already flipped)
+__global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ jobs,
+                                                    const uint64_t* __restrict__ mask,
+                                                    float2* __restrict__ field,
+                                                    float* __restrict__ inten,
+                                                    const float2* __restrict__ hpsf,
+                                                    const int32_t* __restrict__ accept_flag, int N,
+                                                    int P, int G, float vb) {
+  const int j = blockIdx.y;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0 || accept_flag[j] == 0) return;
+  const int CH = G * P;
+  const int g = jb.group;
+  const int r = jb.flip_pix / N, col = jb.flip_pix % N;
+  const float delta = flip_delta(mask, jb, N, P, CH, vb, true);
+  const float invp = 1.0f / (float)P;
+  const size_t hw = (size_t)N * N;
+  float4* U = reinterpret_cast<float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
+  float4* I = reinterpret_cast<float4*>(inten + ((size_t)jb.env * G + g) * hw);
+  const float2* h = hpsf + (size_t)g * hw;
+  const int nq = (int)(hw / 4);
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
+    const int y = (4 * q) / N, x0 = (4 * q) % N;
+    float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+    float4 iv = I[q];
+    const float2* hrow = h + (size_t)((y - r) & (N - 1)) * N;
+    const float2 h0 = hrow[(x0 - col) & (N - 1)], h1 = hrow[(x0 + 1 - col) & (N - 1)];
+    const float2 h2 = hrow[(x0 + 2 - col) & (N - 1)], h3 = hrow[(x0 + 3 - col) & (N - 1)];
+    float uu[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
+    const float hh[8] = {h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
+    float ii[4] = {iv.x, iv.y, iv.z, iv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float ur = uu[2 * k], ui = uu[2 * k + 1];
+      const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
+      const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
+      ii[k] = fmaf(d, invp, ii[k]);
+      uu[2 * k] = nr;
+      uu[2 * k + 1] = ni;
+    }
+    U[2 * q] = make_float4(uu[0], uu[1], uu[2], uu[3]);
+    U[2 * q + 1] = make_float4(uu[4], uu[5], uu[6], uu[7]);
+    I[q] = make_float4(ii[0], ii[1], ii[2], ii[3]);
+  }
+}
+
+hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
+                           const float2* field, const float* inten, const float* target,
+                           const double* chan_stats, hipStream_t st) {
+  PassTimer* tm = pd.timer;
+  if (tm) tm->begin(3, st);
+  hipLaunchKernelGGL(k_psf_eval, dim3(kPsfBlocks, n_jobs), dim3(256), 0, st, jobs, mask, field, inten,
+                     target, pd.hpsf, pd.N, pd.P, pd.G, pd.vb, pd.psf_partial);
+  if (tm) tm->end(3, n_jobs, st);
+  hipLaunchKernelGGL(k_psf_reduce, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, pd.psf_partial,
+                     n_jobs, pd.G, chan_stats, pd.job_stats);
+  return hipGetLastError();
+}
+
+hipError_t launch_psf_commit(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
+                             float2* field, float* inten, const int32_t* accept_flag, hipStream_t st) {
+  PassTimer* tm = pd.timer;
+  if (tm) tm->begin(4, st);
+  hipLaunchKernelGGL(k_psf_commit, dim3(kPsfBlocks, n_jobs), dim3(256), 0, st, jobs, mask, field, inten,
+                     pd.hpsf, accept_flag, pd.N, pd.P, pd.G, pd.vb);
+  if (tm) tm->end(4, n_jobs, st);
+  return hipGetLastError();
+}
+
+}  // namespace hbx

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -26,9 +26,10 @@ EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
     "hbx_plan_workspace_bytes", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
+    "hbx_env_step_psf", "hbx_field_refresh",
 )
-NUM_PASSES = 3
-PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv")
+NUM_PASSES = 5
+PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
 
 
 class HbxError(RuntimeError):
@@ -53,6 +54,7 @@ class EnvBuffers(C.Structure):
         ("chan_stats", C.c_void_p), ("init_psnr", C.c_void_p), ("prev_psnr", C.c_void_p),
         ("max_psnr_diff", C.c_void_p), ("steps", C.c_void_p), ("flip_count", C.c_void_p),
         ("sustained", C.c_void_p), ("intensity", C.c_void_p), ("error", C.c_void_p),
+        ("field", C.c_void_p),
     ]
 
 
@@ -84,6 +86,9 @@ def _declare(lib):
     lib.hbx_step.argtypes = [VP, VP, VP, I32, VP, VP, VP, VP, VP, I32, VP]
     lib.hbx_eval_flips.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP]
     lib.hbx_commit_flip.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP]
+    lib.hbx_env_step_psf.argtypes = [VP, C.POINTER(EnvBuffers), C.POINTER(EnvParams), I32, VP, VP, VP,
+                                     VP, VP, VP, VP]
+    lib.hbx_field_refresh.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]

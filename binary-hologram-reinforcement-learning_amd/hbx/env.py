@@ -33,9 +33,13 @@ class EnvState:
     """Device buffers of B environments (env.py:65-81 attributes)."""
 
     def __init__(self, plan: Plan, n_env: int, keep_record: bool = True, keep_pre_model: bool = True,
-                 keep_intensity: bool = True):
+                 keep_intensity: bool = True, keep_field: bool = False):
         c, dev = plan.cfg, plan.device
         self.plan, self.n = plan, n_env
+        keep_intensity = keep_intensity or keep_field   # the incremental mode needs both
+        # complex64 field of every plane, as float32 pairs (incremental-field mode)
+        self.field = torch.zeros((n_env, c.channels, c.height, c.width, 2), dtype=torch.float32,
+                                 device=dev) if keep_field else None
         self.mask = torch.zeros(plan.mask_shape(n_env), dtype=torch.int64, device=dev)
         self.record = torch.zeros((n_env, c.channels, c.height, c.width), dtype=torch.int8,
                                   device=dev) if keep_record else None
@@ -61,6 +65,7 @@ class EnvState:
         b.chan_stats, b.init_psnr, b.prev_psnr = p(self.chan_stats), p(self.init_psnr), p(self.prev_psnr)
         b.max_psnr_diff, b.steps, b.flip_count = p(self.max_psnr_diff), p(self.steps), p(self.flip_count)
         b.sustained, b.intensity, b.error = p(self.sustained), p(self.intensity), p(self.error)
+        b.field = p(self.field)
 
     def check_error(self):
         if int(self.error.item()) != 0:
@@ -75,6 +80,12 @@ class HologramVecEnv:
     pre_model_fn(target[1, G, H, W]) -> pre-model output [1, CH, H, W] in [0, 1]
     (env.py:106-120: the binary state is pre_model >= 0.5), or
     pre_model_source(i) -> the same for env i directly (injected / synthetic).
+
+    mode="fft" (default) re-propagates the touched colour group every step,
+    exactly as the reference does.  mode="psf" is the incremental-field mode
+    (include/hbx.h hbx_env_step_psf): same results within fp32 tolerance, one
+    streaming pass over the touched plane's cached field instead of 2-D FFTs;
+    the cached fields are re-propagated exactly every ``refresh_every`` steps.
     """
 
     def __init__(self, cfg: OpticsConfig, num_envs: int, target_source: Callable,
@@ -82,9 +93,18 @@ class HologramVecEnv:
                  T_steps: int = 1, T_PSNR_DIFF: float = 0.1, reward_weight: float = RW,
                  accept_rule: int = _lib.ACCEPT_ENV, max_jobs: Optional[int] = None,
                  obs_keys: Sequence[str] = OBS_KEYS, auto_reset: bool = True,
-                 device: Optional[int] = None, pre_model_source: Optional[Callable] = None):
+                 device: Optional[int] = None, pre_model_source: Optional[Callable] = None,
+                 mode: str = "fft", refresh_every: int = 2048):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
+        if mode not in ("fft", "psf"):
+            raise ValueError(f"mode must be 'fft' or 'psf', got {mode!r}")
+        if mode == "psf" and "recon_image" in obs_keys:
+            raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
+                             "drop it from obs_keys or use mode='fft'")
+        self.mode = mode
+        self.refresh_every = int(refresh_every)
+        self._since_refresh = 0
         self.cfg = cfg
         self.num_envs = int(num_envs)
         self.plan = Plan(cfg, max_jobs=max_jobs or max(self.num_envs, cfg.groups), device=device)
@@ -96,7 +116,8 @@ class HologramVecEnv:
         self.state = EnvState(self.plan, self.num_envs,
                               keep_record=True,
                               keep_pre_model="pre_model" in self.obs_keys,
-                              keep_intensity="recon_image" in self.obs_keys)
+                              keep_intensity="recon_image" in self.obs_keys,
+                              keep_field=(mode == "psf"))
         self.target_source = target_source
         self.pre_model_fn = pre_model_fn
         self.pre_model_source = pre_model_source
@@ -173,9 +194,22 @@ class HologramVecEnv:
                                       else actions).to(self.device, torch.int64)
         actions = actions.reshape(self.num_envs).contiguous()
         self._last_actions = actions
-        self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, self._reward, self._psnr,
-                           self._acc, self._term, self._trunc, self._ginten)
+        if self.mode == "psf":
+            self.plan.env_step_psf(self.state.bufs, self.params, self.num_envs, actions, self._reward,
+                                   self._psnr, self._acc, self._term, self._trunc)
+            self._since_refresh += 1
+            if self.refresh_every and self._since_refresh >= self.refresh_every:
+                self.refresh()
+        else:
+            self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, self._reward,
+                               self._psnr, self._acc, self._term, self._trunc, self._ginten)
         return self._reward, self._psnr, self._acc, self._term, self._trunc
+
+    def refresh(self):
+        """Exact FFT re-propagation of the cached fields (incremental mode)."""
+        if self.mode == "psf":
+            self.plan.field_refresh(self.state.bufs, self.num_envs)
+            self._since_refresh = 0
 
     def step(self, actions):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset."""

@@ -234,6 +234,17 @@ class Plan:
         _lib.check(self.lib.hbx_env_reset(self._h, C.byref(bufs), n_env, _ptr(env_ids), n_ids,
                                           _stream(stream)), "hbx_env_reset")
 
+    def env_step_psf(self, bufs, params, n_env, actions, reward, psnr, accepted, terminated, truncated,
+                     stream=None):
+        _lib.check(self.lib.hbx_env_step_psf(self._h, C.byref(bufs), C.byref(params), n_env, _ptr(actions),
+                                             _ptr(reward), _ptr(psnr), _ptr(accepted), _ptr(terminated),
+                                             _ptr(truncated), _stream(stream)), "hbx_env_step_psf")
+
+    def field_refresh(self, bufs, n_env, env_ids: Optional[torch.Tensor] = None, stream=None):
+        n_ids = 0 if env_ids is None else int(env_ids.shape[0])
+        _lib.check(self.lib.hbx_field_refresh(self._h, C.byref(bufs), n_env, _ptr(env_ids), n_ids,
+                                              _stream(stream)), "hbx_field_refresh")
+
     def env_step(self, bufs, params, n_env, actions, reward, psnr, accepted, terminated, truncated,
                  group_intensity=None, stream=None):
         _lib.check(self.lib.hbx_env_step(self._h, C.byref(bufs), C.byref(params), n_env, _ptr(actions),

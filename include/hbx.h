@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 1
+#define HBX_ABI_VERSION 2
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -84,8 +84,11 @@ typedef struct hbx_env_buffers {
   int64_t* steps;          /* [B]                env.steps                    */
   int64_t* flip_count;     /* [B]                env.flip_count               */
   int64_t* sustained;      /* [B]                env.psnr_sustained_steps     */
-  float* intensity;        /* [B][G][H][W] cached group means (nullable)      */
+  float* intensity;        /* [B][G][H][W] cached group means (nullable;
+                              required by the incremental-field mode)          */
   int32_t* error;          /* [1] sticky device error word (nullable)         */
+  float* field;            /* [B][G*P][H][W][2] complex64 propagated field of
+                              every plane (nullable; incremental-field mode)   */
 } hbx_env_buffers_t;
 
 /* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
@@ -128,8 +131,9 @@ int hbx_psnr(hbx_plan_t plan, const double* chan_stats, int32_t n_env, double* p
 
 /* Env reset tail (env.py:120-133): given env.mask already thresholded and
  * env.target set for the listed envs (env_ids nullable = all n_env), propagate
- * every group, fill chan_stats / intensity, set init_psnr = prev_psnr and zero
- * steps / flip_count / sustained / record, max_psnr_diff = -inf. */
+ * every group, fill chan_stats / intensity (and env.field when non-null),
+ * set init_psnr = prev_psnr and zero steps / flip_count / sustained / record,
+ * max_psnr_diff = -inf. */
 int hbx_env_reset(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
                   const int32_t* env_ids, int32_t n_ids, void* stream);
 
@@ -170,6 +174,25 @@ int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stat
                     double* prev_psnr, const int64_t* flips, const double* psnr_out,
                     const double* group_stats, const int32_t* k, void* stream);
 
+/* Incremental-field ("PSF") mode (reported separately from
+ * the FFT-mode headline).  tt.simulate is linear, so flipping pixel (c, r, col)
+ * changes only plane c's field, by delta * h_g shifted to (r, col), where
+ * h_g = IFFT2(H_g) is the single-pixel field and delta = vb * (1 - 2 bit_old):
+ *   U_c' = U_c + delta h_g(y - r, x - col),  I_g' = I_g + (|U_c'|^2 - |U_c|^2) / P
+ * The step streams U_c, I_g and the target channel once (no FFT), then the
+ * same reward / accept / rollback tail as hbx_env_step; accepted steps
+ * rewrite U_c and I_g.  Requires env->field and env->intensity, filled by
+ * hbx_env_reset (or hbx_field_refresh) with the exact FFT path. */
+int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_env_params_t* params,
+                     int32_t n_env, const int64_t* actions, double* reward, double* psnr,
+                     uint8_t* accepted, uint8_t* terminated, uint8_t* truncated, void* stream);
+
+/* Exact re-propagation (FFT path) of env->field, env->intensity and
+ * env->chan_stats for the listed envs (bounds the fp32 drift of the
+ * incremental updates; counters and PSNR history are left untouched). */
+int hbx_field_refresh(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
+                      const int32_t* env_ids, int32_t n_ids, void* stream);
+
 /* Optional device timing of the three propagation passes (hipEvents recorded
  * on the launch stream around every pass launch; not for graph capture).
  * capacity = max launches recorded per pass before hbx_plan_read_timing;
@@ -177,7 +200,9 @@ int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stat
 #define HBX_PASS_ROWFWD 0
 #define HBX_PASS_COL 1
 #define HBX_PASS_ROWINV 2
-#define HBX_NUM_PASSES 3
+#define HBX_PASS_PSF_EVAL 3
+#define HBX_PASS_PSF_COMMIT 4
+#define HBX_NUM_PASSES 5
 int hbx_plan_set_timing(hbx_plan_t plan, int32_t capacity);
 /* Waits for the recorded events; ms_total[HBX_NUM_PASSES] = summed kernel
  * time, launches[HBX_NUM_PASSES], jobs[HBX_NUM_PASSES] = summed jobs per

@@ -270,3 +270,68 @@ def test_dbs_early_stop():
     assert res.stopped_early
     assert res.steps == len(acc)
     assert abs(res.final_psnr - final) <= PSNR_TOL
+
+
+# -- incremental-field (PSF) mode --------------------------------------------------------------
+def test_psf_env_trace_golden(golden_dir):
+    from hbx.env import HologramVecEnv
+    d = load(golden_dir, "env_trace_64.npz")
+    ms, tp, ts, td = d["params"]
+    env = HologramVecEnv(dev_cfg(small_rgb()), 1, lambda i: d["target"],
+                         pre_model_source=lambda i: d["pre_model"], max_steps=int(ms), T_PSNR=float(tp),
+                         T_steps=int(ts), T_PSNR_DIFF=float(td), auto_reset=False, mode="psf",
+                         obs_keys=("state", "target_image"), refresh_every=64)
+    env.reset()
+    for k, a in enumerate(d["actions"]):
+        r, ps, acc, term, trunc = env.step_device(torch.tensor([int(a)], device="cuda"))
+        assert abs(float(ps[0]) - float(d["psnr"][k])) <= PSNR_TOL, k
+        assert (bool(acc[0]), bool(term[0]), bool(trunc[0])) == (
+            bool(d["accepted"][k]), bool(d["terminated"][k]), bool(d["truncated"][k])), k
+    assert np.array_equal(env.state.mask[0].cpu().numpy().view("<u8"), d["final_mask_bits"])
+    assert np.array_equal(env.state.record[0].cpu().numpy(), d["final_record"])
+
+
+def test_psf_field_matches_oracle():
+    from hbx.env import HologramVecEnv
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 4)
+    env = HologramVecEnv(dev_cfg(ocfg), 1, lambda i: tgt, pre_model_source=lambda i: pre, mode="psf",
+                         obs_keys=(), auto_reset=False)
+    env.reset()
+    mask = (pre >= 0.5).astype(np.uint8)
+    prop = O.Propagator(ocfg)
+    for g in range(3):
+        u = O.propagate(O.mask_to_field(mask[2 * g:2 * g + 2]), prop.h[g])
+        got = env.state.field[0, 2 * g:2 * g + 2].cpu().numpy()
+        got = got[..., 0] + 1j * got[..., 1]
+        assert np.max(np.abs(got - u)) <= 2e-5 * np.max(np.abs(u))
+        assert np.allclose(env.state.intensity[0, g].cpu().numpy(), prop.group_intensity(mask, g),
+                           atol=2e-5 * np.max(np.abs(u)) ** 2)
+
+
+@pytest.mark.parametrize("field_kind", [O.FIELD_AMPLITUDE, O.FIELD_PHASE])
+def test_psf_matches_fft_full_size(field_kind):
+    """1024 x 24, 4 envs, 40 steps: the incremental mode and the FFT mode agree."""
+    import hbx
+    from hbx.env import HologramVecEnv
+    cfg = hbx.rgb_config(1024, field_kind=field_kind)
+    B = 4
+    gens = [torch.Generator(device="cuda").manual_seed(50 + i) for i in range(B)]
+    pres = [torch.rand((24, 1024, 1024), generator=g, device="cuda") for g in gens]
+    tgts = [torch.rand((3, 1024, 1024), generator=g, device="cuda") for g in gens]
+    kw = dict(pre_model_source=lambda i: pres[i], obs_keys=(), auto_reset=False)
+    fft = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    psf = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="psf", refresh_every=16, **kw)
+    fft.reset()
+    psf.reset()
+    assert torch.allclose(fft.state.init_psnr, psf.state.init_psnr, atol=1e-9)
+    acts = torch.randint(0, 24 * 1024 * 1024, (40, B), generator=gens[0], device="cuda")
+    for k in range(40):
+        _, p1, a1, _, _ = fft.step_device(acts[k])
+        _, p2, a2, _, _ = psf.step_device(acts[k])
+        assert torch.max(torch.abs(p1 - p2)).item() <= PSNR_TOL
+        d = torch.abs(p1 - fft.state.prev_psnr)
+        assert torch.equal(a1, a2) or bool((d < 1e-5).any())
+    assert torch.equal(fft.state.mask, psf.state.mask)
+    fft.close()
+    psf.close()
