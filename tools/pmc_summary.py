@@ -14,7 +14,7 @@ import os
 import re
 from collections import defaultdict
 
-KERNELS = ("k_rowfwd", "k_col", "k_rowinv")
+KERNELS = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
 
 
 def short(name):
@@ -63,7 +63,8 @@ def main():
     a = ap.parse_args()
     N, P = a.N, a.P
     alg = {"k_rowfwd": P * N * N // 8 + P * N * N * 4, "k_col": P * N * N * 12,
-           "k_rowinv": P * N * N * 8 + N * N * 4}
+           "k_rowinv": P * N * N * 8 + N * N * 4, "k_psf_eval": 16 * N * N,
+           "k_psf_commit": 24 * N * N}   # commit: per ACCEPTED job
     trace = load_trace(os.path.join(a.dir, "trace", "run_kernel_trace.csv"))
     cnt = {}
     for sub in ("fetch", "write", "sq", "lds"):
