@@ -160,9 +160,11 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
   if (hipMalloc(&pd.psf_partial, (size_t)max_jobs * hbx::kPsfBlocks * 2 * sizeof(double)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "psf partials");
+  if (hipMalloc(&pd.zero_row, (size_t)N * sizeof(float)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "zero row");
   if (hipMemcpy(pd.tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess)
+      hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess ||
+      hipMemset(pd.zero_row, 0, (size_t)N * sizeof(float)) != hipSuccess)
     return cleanup(HBX_ERR_HIP, "table upload");
   *out = p;
   return HBX_OK;
@@ -183,6 +185,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->err) (void)hipFree(p->err);
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
+  if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   hbx_plan_set_timing(p, 0);
   delete p;
   return HBX_OK;
@@ -303,11 +306,11 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
     HBX_HIP(hbx::launch_jobs_full(env_ids ? env_ids + i0 : nullptr, n, G, p->jobs, st));
     const size_t mwords = (size_t)G * pd.P * pd.N * (pd.N / 64);
     const uint64_t* m = env_ids ? mask : mask + (size_t)i0 * mwords;
-    const float* tg = env_ids ? target : target + (size_t)i0 * G * pd.N * pd.N;
+    const float* tg = (env_ids || !target) ? target : target + (size_t)i0 * G * pd.N * pd.N;
     float2* fo = field ? (env_ids ? field : field + (size_t)i0 * G * pd.P * pd.N * pd.N) : nullptr;
     HBX_HIP(hbx::run_jobs(pd, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
                           intensity ? p->job_inten : nullptr, fo, st));
-    double* cs = env_ids ? chan_stats : chan_stats + (size_t)i0 * G * 3;
+    double* cs = (env_ids || !chan_stats) ? chan_stats : chan_stats + (size_t)i0 * G * 3;
     double* ps = psnr ? (env_ids ? psnr : psnr + i0) : nullptr;
     EnvDev ed = dummy;
     if (env) ed = env_ids ? *env : env_offset(*env, i0, G * pd.P, G, pd.N);
@@ -335,6 +338,17 @@ int hbx_propagate(hbx_plan_t p, const uint64_t* mask, const float* target, int32
   HBX_HIP(hipSetDevice(p->device));
   return propagate_full(p, mask, target, nullptr, n_env, intensity, chan_stats, psnr, nullptr,
                         nullptr, (hipStream_t)stream);
+}
+
+int hbx_simulate(hbx_plan_t p, const uint64_t* mask, int32_t n_env, float* field, float* intensity,
+                 void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!mask || !field || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
+  if (n_env == 0) return HBX_OK;
+  HBX_HIP(hipSetDevice(p->device));
+  return propagate_full(p, mask, nullptr, nullptr, n_env, intensity, nullptr, nullptr, nullptr,
+                        reinterpret_cast<float2*>(field), (hipStream_t)stream);
 }
 
 int hbx_psnr(hbx_plan_t p, const double* chan_stats, int32_t n_env, double* psnr, void* stream) {

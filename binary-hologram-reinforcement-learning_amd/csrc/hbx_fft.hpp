@@ -157,6 +157,9 @@ __device__ __forceinline__ void fft_group(float2 (&v)[R], int t, const Scratch& 
   // keep the twiddle loads local to each FFT: without this barrier the
   // compiler CSEs / hoists them across calls and pins 2R VGPRs for good
   asm volatile("" ::: "memory");
+#ifdef HBX_NO_FFT  // access-pattern ceiling experiments only (tools/): data moves, no arithmetic
+  return;
+#endif
   dft_reg<R, INV>(v);
 #pragma unroll
   for (int k1 = 1; k1 < R; ++k1) {

@@ -96,8 +96,10 @@ __global__ void k_full_finalize(const JobDesc* __restrict__ jobs, const double* 
   double sxy = 0.0, sxx = 0.0, syy = 0.0;
   for (int g = 0; g < G; ++g) {
     const double* s = job_stats + 3 * (size_t)(i * G + g);
-    double* d = chan_stats + ((size_t)e * G + g) * 3;
-    d[0] = s[0]; d[1] = s[1]; d[2] = s[2];
+    if (chan_stats) {
+      double* d = chan_stats + ((size_t)e * G + g) * 3;
+      d[0] = s[0]; d[1] = s[1]; d[2] = s[2];
+    }
     sxy += s[0]; sxx += s[1]; syy += s[2];
   }
   const double ps = psnr_from(sxy, sxx, syy, count, rel_scale, peak);

@@ -223,7 +223,13 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
     float2 v[R];
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) v[jj] = nxt[jj];
+    const bool dc = (kx == 0);
+    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N;
+#ifdef HBX_EXP_ROLE2_NOLOAD  // timing experiment: only role 1 reads A
+    if (it + 1 < ITER && !role2) {
+#else
     if (it + 1 < ITER) {  // next line in flight under this line's FFTs
+#endif
       const float2* in = ain + (size_t)(kx + LPB) * N;
 #pragma unroll
       for (int jj = 0; jj < R; ++jj) nxt[jj] = in[t + R * jj];
@@ -236,21 +242,23 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 #pragma unroll
     for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
     wave_sync();
-    const bool dc = (kx == 0);
     // a = alpha Z + beta M with per-lane complex coefficients: branch-free
     float2 alpha, beta;
     if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
                   beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
     else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
                   beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
-    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N;
     const int tm = (R - t) & (R - 1);
 #pragma unroll
     for (int k2 = 0; k2 < R; ++k2) {
       // conj F(N - ky): lane tm, register R-1-k2 (lane 0: own register (R-k2) mod R)
       const float2 mm = (t == 0) ? *sc.at(0, (R - k2) & (R - 1)) : *sc.at(tm, R - 1 - k2);
       const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, conjf2(mm)));
+#if defined(HBX_EXP_NOH)  // timing experiment: transfer-function loads removed
+      v[k2] = a;
+#else
       v[k2] = cmul(a, hp[t + R * k2]);
+#endif
     }
     fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
     float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
@@ -269,7 +277,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int G, double* __restrict__ partial,
                                                    float* __restrict__ inten_out,
-                                                   float2* __restrict__ field_out) {
+                                                   float2* __restrict__ field_out,
+                                                   size_t tmask) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // rows per block
   constexpr int RB = N / GPB;
@@ -346,7 +355,9 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
   }
 
   const float invp = 1.0f / (float)P;
-  const float* trow = target + (((size_t)jb.env * G + jb.group) * N + y) * N;
+  // tmask = 0 points every row at the plan's zero row (no target): the loads
+  // stay unconditional, so they issue early like the rest of the stream
+  const float* trow = target + ((((size_t)jb.env * G + jb.group) * N + y) * N & tmask);
   double sxy = 0.0, sxx = 0.0, syy = 0.0;
 #pragma unroll
   for (int k = 0; k < R; ++k) {
@@ -412,8 +423,9 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (N / GPB);
     if (tm) tm->begin(2, st);
-    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target, pd.tw,
-                       P, pd.G, pd.partial, inten_out, field_out);
+    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
+                       target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
+                       field_out, target ? ~(size_t)0 : (size_t)0);
     if (tm) tm->end(2, n_jobs, st);
   }
   hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial,

@@ -182,6 +182,19 @@ class Plan:
                                           _ptr(stats), _ptr(psnr), _stream(stream)), "hbx_propagate")
         return inten, stats, psnr
 
+    def simulate(self, mask: torch.Tensor, want_intensity: bool = False, stream=None):
+        """Complex field of every plane (tt.simulate restated): returns
+        (field complex64 [B, CH, H, W], intensity [B, G, H, W] | None)."""
+        n = mask.shape[0]
+        c = self.cfg
+        _need(mask, "mask", torch.int64, self.mask_shape(n), self.device)
+        field = torch.empty((n, c.channels, c.height, c.width, 2), dtype=torch.float32, device=self.device)
+        inten = torch.empty((n, c.groups, c.height, c.width), dtype=torch.float32,
+                            device=self.device) if want_intensity else None
+        _lib.check(self.lib.hbx_simulate(self._h, _ptr(mask), n, _ptr(field), _ptr(inten), _stream(stream)),
+                   "hbx_simulate")
+        return torch.view_as_complex(field), inten
+
     def psnr(self, chan_stats: torch.Tensor, stream=None) -> torch.Tensor:
         n = chan_stats.shape[0]
         _need(chan_stats, "chan_stats", torch.float64, (n, self.cfg.groups, 3), self.device)

@@ -124,6 +124,13 @@ size_t hbx_plan_workspace_bytes(hbx_plan_t plan);
 int hbx_propagate(hbx_plan_t plan, const uint64_t* mask, const float* target, int32_t n_env,
                   float* intensity, double* chan_stats, double* psnr, void* stream);
 
+/* tt.simulate(tt.Tensor(mask, meta), z) (env.py:170-172; DBS_1024_24.py:
+ * 326-328) for binary masks: the propagated complex field of every plane,
+ *   field[B][G*P][H][W][2] = IFFT2(FFT2(u) H_g)   (complex64, re/im pairs)
+ * and optionally the plane-mean intensity[B][G][H][W] (nullable). */
+int hbx_simulate(hbx_plan_t plan, const uint64_t* mask, int32_t n_env, float* field,
+                 float* intensity, void* stream);
+
 /* PSNR from per-channel statistics (tt.relativeLoss(.., tm.get_PSNR),
  * env.py:174): chan_stats[B][G][3] -> psnr[B]. */
 int hbx_psnr(hbx_plan_t plan, const double* chan_stats, int32_t n_env, double* psnr,

@@ -30,6 +30,29 @@ __global__ void k_r1w2(const float4* __restrict__ a, float4* __restrict__ b, siz
   }
 }
 
+// 8 B per lane (float2): the column pass's access width
+__global__ void k_read8(const float2* __restrict__ a, size_t n, float* out) {
+  float2 acc = make_float2(0, 0);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float2 v = a[i];
+    acc.x += v.x; acc.y += v.y;
+  }
+  if (acc.x + acc.y == 12345.f) out[0] = 1.f;
+}
+__global__ void k_write8(float2* __restrict__ a, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    a[i] = make_float2(1, (float)i);
+}
+__global__ void k_copy8(const float2* __restrict__ a, float2* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    b[i] = a[i];
+}
+// one element per thread, no grid-stride loop (grid = n / 256)
+__global__ void k_copy_flat(const float4* __restrict__ a, float4* __restrict__ b) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  b[i] = a[i];
+}
+
 int main() {
   const size_t bytes = (size_t)4 << 30;  // 4 GiB per buffer
   const size_t n = bytes / sizeof(float4);
@@ -62,5 +85,14 @@ int main() {
   time("write", (double)bytes, [&] { hipLaunchKernelGGL(k_write, grid, block, 0, 0, a, n); });
   time("copy_r1w1", 2.0 * bytes, [&] { hipLaunchKernelGGL(k_copy, grid, block, 0, 0, a, b, n); });
   time("r1w2", 3.0 * bytes, [&] { hipLaunchKernelGGL(k_r1w2, grid, block, 0, 0, a, b, n); });
+  time("read8", (double)bytes, [&] { hipLaunchKernelGGL(k_read8, grid, block, 0, 0, (const float2*)a, 2 * n, o); });
+  time("write8", (double)bytes, [&] { hipLaunchKernelGGL(k_write8, grid, block, 0, 0, (float2*)a, 2 * n); });
+  time("copy8_r1w1", 2.0 * bytes, [&] { hipLaunchKernelGGL(k_copy8, grid, block, 0, 0, (const float2*)a, (float2*)b, 2 * n); });
+  time("copy_flat_r1w1", 2.0 * bytes, [&] { hipLaunchKernelGGL(k_copy_flat, (unsigned)(n / 256), block, 0, 0, a, b); });
+  for (int g : {1024, 2048, 8192, 16384}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "copy_r1w1_grid%d", g);
+    time(nm, 2.0 * bytes, [&] { hipLaunchKernelGGL(k_copy, g, block, 0, 0, a, b, n); });
+  }
   return 0;
 }
