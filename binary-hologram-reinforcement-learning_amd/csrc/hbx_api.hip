@@ -126,6 +126,18 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       const double a = -2.0 * M_PI * (double)((t * k1) % N) / (double)N;
       tw[(size_t)k1 * R + t] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
+  if (N == 1024) {  // whole-wave FFT tables of the column pass: tw1[k1][L], tw2[m1][l0]
+    for (int k1 = 0; k1 < 16; ++k1)
+      for (int L = 0; L < 64; ++L) {
+        const double a = -2.0 * M_PI * (double)(L * k1) / 1024.0;
+        tw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+      }
+    for (int m1 = 0; m1 < 16; ++m1)
+      for (int l0 = 0; l0 < 4; ++l0) {
+        const double a = -2.0 * M_PI * (double)(l0 * m1) / 64.0;
+        tw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+      }
+  }
   const size_t hrow = (size_t)(N / 2 + 1) * N;
   std::vector<float2> ht((size_t)G * hrow);
   const double scale = 1.0 / ((double)N * (double)N);  // ifft2 normalisation

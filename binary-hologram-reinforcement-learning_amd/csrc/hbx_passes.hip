@@ -237,33 +237,261 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
     fft_group<R, false>(v, t, sc, tw);
 
     // F (natural order: lane t, register k2 -> ky = t + R k2) into the scratch,
-    // then M[k2] = conj F(-ky) read back from lane (R - t) mod R.
-    wave_sync();
+    // then M[k2] = conj F(-ky) read back from lane (R - t) mod R, register
+    // R-1-k2 -- for lane 0 its own register (R - k2) mod R, which the extra
+    // pad-slot copy of v[0] turns into one address per lane (+1 offset).
+    // Only the first block iteration of line block 0 can hold kx = 0, so the
+    // general a = alpha Z + beta M form runs there alone (block-uniform
+    // branch); elsewhere role 1 is a = Z (no M at all) and role 2 a = M.
+    const bool general = (lb == 0 && it == 0);
+    if (general || role2) {
+      wave_sync();
 #pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
-    wave_sync();
-    // a = alpha Z + beta M with per-lane complex coefficients: branch-free
-    float2 alpha, beta;
-    if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
-                  beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
-    else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
-                  beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
-    const int tm = (R - t) & (R - 1);
+      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
+      *sc.at(t, R) = v[0];
+      wave_sync();
+    }
+    const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
+    // H(kx, t + R k2) from two bases 4 KB apart: every load then fits the
+    // 12-bit immediate offset (otherwise the compiler keeps per-k2 64-bit
+    // offsets live across the loop and spills them)
+    const float2* hq = hp + t;
+    const float2* hq2 = hq + 16 * R;
+    auto hload = [&](int k2) { return k2 < 16 ? hq[R * k2] : hq2[R * (k2 - 16)]; };
+    if (general) {
+      float2 alpha, beta;
+      if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
+                    beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
+      else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
+                    beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
 #pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) {
-      // conj F(N - ky): lane tm, register R-1-k2 (lane 0: own register (R-k2) mod R)
-      const float2 mm = (t == 0) ? *sc.at(0, (R - k2) & (R - 1)) : *sc.at(tm, R - 1 - k2);
-      const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, conjf2(mm)));
+      for (int k2 = 0; k2 < R; ++k2) {
+        const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, conjf2(mrow[-k2])));
+        v[k2] = cmul(a, hload(k2));
+      }
+    } else if (role2) {
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) v[k2] = cmul(conjf2(mrow[-k2]), hload(k2));
+    } else {
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) {
 #if defined(HBX_EXP_NOH)  // timing experiment: transfer-function loads removed
-      v[k2] = a;
+        (void)hload;
 #else
-      v[k2] = cmul(a, hp[t + R * k2]);
+        v[k2] = cmul(v[k2], hload(k2));
 #endif
+      }
     }
     fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
     float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
 #pragma unroll
     for (int k2 = 0; k2 < R; ++k2) out[t + R * k2] = v[k2];
+  }
+}
+
+// Column pass, one lane group per input line and both of its output lines:
+// forward FFT over y -> Z; Z into the group's scratch, M = conj Z(-ky) read
+// back into registers; both multiplied by the same H(kx, .) row (H is even
+// in fx); inverse FFT of Z H -> B line kx, then of M H -> B line N - kx
+// (kx = 0: (Z + M)/2 -> line 0 and -i (Z - M)/2 with the H(N/2) row -> line
+// N/2).  One forward FFT per input line instead of one per output line (the
+// two-role k_col), one A read, one H read, and no cross-group traffic: every
+// LDS hand-off stays inside the group's own scratch (wave_sync only).  The
+// next line's loads go into v as soon as line kx is stored and fly under the
+// second inverse FFT.
+template <int R>
+__host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
+
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
+                                                 const float2* __restrict__ ws_a,
+                                                 float2* __restrict__ ws_b,
+                                                 const float2* __restrict__ htab,
+                                                 const float2* __restrict__ tw_glob, int P) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;          // lane groups (= input lines) per block iteration
+  constexpr int ITER = col2_iters<R>();
+  constexpr int LB = (N / 2) / (GPB * ITER);
+  static_assert((N / 2) % (GPB * ITER) == 0, "line blocking");
+  __shared__ float2 tw[N];
+  __shared__ float2 scratch[GPB * R * (R + 1)];
+
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  int bid = blockIdx.x;
+  const int lb = bid % LB;
+  bid /= LB;
+  const int p = bid % P;
+  const int j = bid / P;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;
+  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N + t;
+  float2* bout = ws_b + ((size_t)j * P + p) * N * N + t;
+  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N + t;
+  const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+  const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
+  const int kx0 = lb * (GPB * ITER) + grp;
+
+  float2 v[R];
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) v[jj] = ain[(size_t)kx0 * N + R * jj];
+  lds_barrier();  // tw visible (the line loads stay in flight)
+
+#pragma unroll 1
+  for (int it = 0; it < ITER; ++it) {
+    const int kx = kx0 + it * GPB;
+    const bool dc = (kx == 0);
+    fft_group<R, false>(v, t, sc, tw);
+    // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
+    // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
+    // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
+    // R-1-k2, or for lane 0 its own register (R - k2) mod R.  Each H value is
+    // consumed as it arrives, so H never needs a register array of its own.
+    const float2* hrow = hg + (size_t)kx * N;
+    wave_sync();
+    if (!dc) {
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) {
+        const float2 h = hrow[R * k2];
+        const float2 w = cmulc(v[k2], h);
+        *sc.at(t, k2) = w;
+        if (k2 == 0) *sc.at(t, R) = w;
+        v[k2] = cmul(v[k2], h);
+      }
+    } else {  // kx = 0: one group of the whole plane; plain Z through the scratch
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
+      *sc.at(t, R) = v[0];
+    }
+    wave_sync();
+    float2 m[R];
+#pragma unroll
+    for (int k2 = 0; k2 < R; ++k2) m[k2] = conjf2(mrow[-k2]);
+    if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
+      const float2* hnyq = hg + (size_t)(N / 2) * N;
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) {
+        const float2 z = v[k2], mm = m[k2];
+        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), hrow[R * k2]);
+        m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), hnyq[R * k2]);
+      }
+    }
+    fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
+    {
+      float2* out = bout + (size_t)kx * N;
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = v[k2];
+    }
+    if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
+      const float2* in = ain + (size_t)(kx + GPB) * N;
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) v[jj] = in[R * jj];
+    }
+    fft_group<R, true>(m, t, sc, tw);
+    {
+      float2* out = bout + (size_t)(dc ? N / 2 : N - kx) * N;
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = m[k2];
+    }
+  }
+}
+
+// N = 1024 column pass on whole-wave FFTs (hbx_fft.hpp): one line per wave,
+// 16 values per lane.  Same two-role scheme as k_col (waves 0, 1 role 1 on lines
+// kx, kx + 1; waves 2, 3 role 2 on the same input lines), but a lane holds a
+// quarter of the registers of the 32-lane version, so the next A line, this
+// line's transfer-function row and the line itself are all in flight at three
+// workgroups (12 waves) per CU: 43 KB of LDS, <= 168 VGPRs.
+// The spectrum stays in slot order (ky = wave_ky_base(L) + 16 m1) between the
+// forward and inverse FFTs; H is read in that order.  M = conj F(-ky) goes
+// through the wave's scratch in natural order, padded every 256 entries.
+__device__ __forceinline__ int mpad(int ky) { return ky + ((ky >> 8) << 3); }
+
+constexpr int kColWaveIter = 4;   // lines per wave
+constexpr int kColWaveLines = 2 * kColWaveIter;   // input lines per workgroup
+
+__global__ __launch_bounds__(256, 3) void k_col_w(const JobDesc* __restrict__ jobs,
+                                                  const float2* __restrict__ ws_a,
+                                                  float2* __restrict__ ws_b,
+                                                  const float2* __restrict__ htab,
+                                                  const float2* __restrict__ tww, int P) {
+  constexpr int N = 1024;
+  constexpr int LB = (N / 2) / kColWaveLines;
+  __shared__ float2 tw1[1024];
+  __shared__ float2 tw2[64];
+  __shared__ __attribute__((aligned(16))) float2 scratch[4 * kWaveScratch];
+  for (int i = threadIdx.x; i < 1024 + 64; i += 256) {
+    if (i < 1024) tw1[i] = tww[i];
+    else tw2[i - 1024] = tww[i];
+  }
+  const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+  const bool role2 = w >= 2;
+  int bid = blockIdx.x;
+  const int lb = bid % LB;
+  bid /= LB;
+  const int p = bid % P;
+  const int j = bid / P;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;  // uniform per block
+  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N;
+  float2* bout = ws_b + ((size_t)j * P + p) * N * N;
+  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N;
+  float2* scr = scratch + w * kWaveScratch;
+  const int kyb = wave_ky_base(L);
+  const int kx0 = lb * kColWaveLines + (w & 1);
+
+  float2 nxt[16];
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) nxt[jj] = ain[(size_t)kx0 * N + L + 64 * jj];
+  lds_barrier();  // tables visible (the line loads stay in flight)
+
+  // fully unrolled: nxt and v swap registers instead of being copied (a copy
+  // forces an early wait on the prefetch), and with no loop back-edge the
+  // vmcnt waits are exact (a merge point makes them count the previous line's
+  // stores too)
+#pragma unroll
+  for (int it = 0; it < kColWaveIter; ++it) {
+    const int kx = kx0 + 2 * it;
+    const bool dc = (kx == 0);
+    float2 v[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) v[jj] = nxt[jj];
+    // this line's H row (slot order) lands under the forward FFT
+    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N + kyb;
+    float2 h[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) h[m] = hp[16 * m];
+    {  // next line in flight under both FFTs.  Unconditional (the last
+       // iteration re-reads its own line from L2): a conditional prefetch
+       // makes the H wait below a vmcnt(0) that also waits for this line.
+      const int kn = (it + 1 < kColWaveIter) ? kx + 2 : kx;
+      const float2* in = ain + (size_t)kn * N + L;
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) nxt[jj] = in[64 * jj];
+    }
+    wave_fft1024_fwd(v, L, scr, tw1, tw2);
+
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) scr[mpad(kyb + 16 * m)] = v[m];
+    wave_sync();
+    float2 alpha, beta;   // a = alpha Z + beta M (see k_col)
+    if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
+                  beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
+    else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
+                  beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const float2 mm = scr[mpad((N - (kyb + 16 * m)) & (N - 1))];
+      const float2 a = cadd(cmul(alpha, v[m]), cmul(beta, conjf2(mm)));
+      v[m] = cmul(a, h[m]);
+    }
+    wave_fft1024_inv(v, L, scr, tw1, tw2);   // its first scratch write follows a wave_sync
+    float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N + L;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) out[64 * jj] = v[jj];
   }
 }
 
@@ -413,11 +641,28 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if (tm) tm->end(0, n_jobs, st);
   }
   {
-    constexpr int LINES_PER_BLOCK = (GPB / 2) * col_iters<R>();
-    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
     if (tm) tm->begin(1, st);
-    hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
-                       pd.tw, P);
+#ifdef HBX_COL_WAVE   // A/B switch: whole-wave FFT column pass at N = 1024
+    if constexpr (N == 1024) {
+#else
+    if constexpr (false) {
+#endif
+      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / kColWaveLines);
+      hipLaunchKernelGGL(k_col_w, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
+                         pd.htab, pd.tw + N, P);
+    } else {
+#ifdef HBX_COL_ROLES   // A/B switch: the two-role column pass
+      constexpr int LINES_PER_BLOCK = (GPB / 2) * col_iters<R>();
+      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
+      hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
+                         pd.htab, pd.tw, P);
+#else
+      constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
+      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
+      hipLaunchKernelGGL(k_col2<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
+                         pd.htab, pd.tw, P);
+#endif
+    }
     if (tm) tm->end(1, n_jobs, st);
   }
   {
