@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--psf-steps", type=int, default=200)
     ap.add_argument("--chunk", type=int, default=0,
                     help="jobs per launch sequence (0 = all envs at once)")
+    ap.add_argument("--dbs-flips", type=int, default=8192,
+                    help="greedy-DBS prefix (flips of the shuffled order) timed on env 0's image, "
+                         "SURVEY 8d cfg 2 (0 = skip)")
+    ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")
     return ap.parse_args()
 
 
@@ -65,6 +69,72 @@ def algorithmic_bytes(N: int, P: int):
             "k_rowinv": P * N * N * 8 + N * N * 4,
             "k_psf_eval": 16 * N * N,
             "k_psf_commit": 24 * N * N}
+
+
+def canonical_step_bytes(N: int, P: int) -> int:
+    """SURVEY 8d's canonical bytes per FFT-mode env-step: two complex64 read+write
+    round trips per plane + the touched target channel + the bit-packed mask."""
+    return P * 4 * (8 * N * N) + 4 * N * N + P * N * N // 8
+
+
+def cpu_baseline_scipy(n_steps: int, N: int, workers: int):
+    """SURVEY 8d's second CPU figure: the same env-step with scipy.fft complex64
+    over `workers` threads (numpy oracle for everything but the transforms)."""
+    import numpy as np
+    import scipy.fft as sf
+    from oracle import hbx_oracle as O
+    cfg = O.rgb_config(N)
+    pre, tgt = O.synthetic_inputs(cfg, 0)
+    h = [cfg.transfer(g).astype(np.complex64) for g in range(cfg.groups)]
+    mask = (pre >= 0.5).astype(np.int8)
+    rng = np.random.default_rng(2)
+    acts = rng.integers(0, cfg.channels * N * N, n_steps + 2)
+
+    def step(a):
+        c, r, col = O.decode_action(int(a), N, N)
+        mask[c, r, col] ^= 1
+        g = c // cfg.planes
+        u = mask[g * cfg.planes:(g + 1) * cfg.planes].astype(np.complex64)
+        f = sf.ifft2(sf.fft2(u, axes=(-2, -1), workers=workers) * h[g], axes=(-2, -1), workers=workers)
+        inten = np.mean(f.real * f.real + f.imag * f.imag, axis=0)
+        return O.chan_stats(inten, tgt[g])
+
+    step(acts[0]); step(acts[1])
+    t0 = time.perf_counter()
+    for a in acts[2:]:
+        step(a)
+    dt = time.perf_counter() - t0
+    return {"value": n_steps / dt, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": f"{n_steps} env-steps, scipy.fft complex64 with workers={workers}, {dt:.1f} s"}
+
+
+def dbs_prefix(cfg, mask, target, n_flips: int):
+    """SURVEY 8d cfg 2: greedy DBS (strict accept, DBS_1024_24.py:313-422) over the
+    first n_flips of rng(3).permutation(CH*N^2) on one image, speculative batches
+    (hbx.dbs.greedy).  Returns flips/s and the extrapolated full-sweep time."""
+    import numpy as np
+    import torch
+    from hbx import dbs
+    from hbx.plan import Plan
+    CH, N = cfg.channels, cfg.height
+    order = np.random.default_rng(3).permutation(CH * N * N)[:n_flips]
+    plan = Plan(cfg, max_jobs=256)
+    m = mask.clone()
+    dbs.greedy(plan, m.clone(), target, order[:256])          # warm-up (plan tables, kernels)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = dbs.greedy(plan, m, target, order)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    plan.close()
+    rate = res.steps / dt
+    return {"flips": res.steps, "seconds": round(dt, 3), "flips_per_s": round(rate, 1),
+            "accepted": len(res.accepted_positions), "launches": res.launches,
+            "psnr_gain_db": round(res.final_psnr - res.initial_psnr, 6),
+            "full_sweep_extrapolated_s": round(CH * N * N / rate, 1),
+            "note": "FFT mode, speculative first-improving batches (serial accept sequence), "
+                    "prefix of the shuffled order; acceptance is highest at the start of a sweep, "
+                    "so the extrapolation is pessimistic"}
 
 
 def cpu_baseline(n_steps: int, N: int):
@@ -208,6 +278,7 @@ def main():
                     "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
         step_bytes = (abytes["k_rowfwd"] + abytes["k_col"] + abytes["k_rowinv"]) * B
+        canon = canonical_step_bytes(N, P)
         out = {
             "metric": "env-steps/sec (1024x1024, 24-plane)",
             "value": round(value, 2),
@@ -229,13 +300,24 @@ def main():
             "roofline": roofline,
             "passes": rounded(passes),
             "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            "step_canonical": {"bytes_per_env_step": canon,
+                               "GBs": round(canon * value / world / 1e9, 1),
+                               "frac": round(canon * value / world / 1e9 / HBM_PEAK_GBS, 4),
+                               "note": "SURVEY 8d canonical traffic (two complex64 round trips per "
+                                       "plane + target + mask) x env-steps/s per GPU, vs 8 TB/s"},
             "accept_rate": round(acc_rate, 4),
         }
         if world == 1 and not args.no_psnr_check:
             out["psnr_delta_vs_numpy"] = psnr_check(vec, N)
+    dbs_mask = vec.state.mask[0].clone()
+    dbs_target = vec.state.target[0].clone()
     vec.close()
     del vec
     torch.cuda.empty_cache()
+
+    if rank == 0 and world == 1 and args.dbs_flips > 0:
+        out["dbs_greedy"] = dbs_prefix(cfg, dbs_mask, dbs_target, args.dbs_flips)
+        torch.cuda.empty_cache()
 
     if not args.no_psf:
         vec, dt, timing, acc_rate = measure("psf", args.psf_steps, max(args.warmup, 5))
@@ -258,6 +340,12 @@ def main():
     if rank == 0:
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, N)
+            if not args.no_scipy:
+                try:
+                    workers = min(16, len(os.sched_getaffinity(0)))
+                    out["cpu_baseline_scipy"] = cpu_baseline_scipy(max(4, args.cpu_sample), N, workers)
+                except Exception as e:  # scipy is optional on the box
+                    out["cpu_baseline_scipy"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
 
 
