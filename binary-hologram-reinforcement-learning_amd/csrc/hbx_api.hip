@@ -51,6 +51,16 @@ struct hbx_plan {
   float* job_inten;       // [max_jobs][N][N]
   int32_t* accept_flag;   // [max_jobs]
   int32_t* err;           // [1]
+  // flip-map workspace (lazy, hbx_flip_map)
+  float2* map_field = nullptr;   // [CH][N][N]
+  float* map_inten = nullptr;    // [G][N][N]
+  double* map_stats = nullptr;   // [G][3] + psnr
+  float2* map_q = nullptr;       // [G][4][N][N] h-side spectra
+  double* map_d4 = nullptr;      // [G]
+  double* map_part = nullptr;    // [G][64]
+  float2* map_x = nullptr;       // [4P + P/2 + 1][N][N]
+  float2* map_s = nullptr;       // same size: FFT scratch
+  float2* map_y = nullptr;       // [P + P/2 + 1][N][N]
 };
 
 namespace {
@@ -198,6 +208,9 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
+  for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
+                  (void*)p->map_d4, (void*)p->map_part, (void*)p->map_x, (void*)p->map_s, (void*)p->map_y})
+    if (q) (void)hipFree(q);
   hbx_plan_set_timing(p, 0);
   delete p;
   return HBX_OK;
@@ -554,6 +567,62 @@ int hbx_eval_flips(hbx_plan_t p, const uint64_t* base_mask, const float* target,
                                       group_stats ? group_stats + (size_t)k0 * 3 : nullptr,
                                       pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
   }
+  return HBX_OK;
+}
+
+namespace {
+int ensure_map(hbx_plan_t p, hipStream_t st) {
+  if (p->map_y) return HBX_OK;
+  int rc = ensure_hpsf(p, st);
+  if (rc) return rc;
+  PlanDev& pd = p->pd;
+  const size_t hw = (size_t)pd.N * pd.N;
+  const int G = pd.G, P = pd.P, CH = G * P;
+  const size_t nx = 4 * P + P / 2 + 1, ny = P + P / 2 + 1;
+  const size_t ns = std::max(nx, (size_t)4 * G);
+  if (hipMalloc(&p->map_field, CH * hw * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&p->map_inten, G * hw * sizeof(float)) != hipSuccess ||
+      hipMalloc(&p->map_stats, (size_t)(3 * G + 1) * sizeof(double)) != hipSuccess ||
+      hipMalloc(&p->map_q, (size_t)4 * G * hw * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&p->map_d4, (size_t)G * sizeof(double)) != hipSuccess ||
+      hipMalloc(&p->map_part, (size_t)G * 64 * sizeof(double)) != hipSuccess ||
+      hipMalloc(&p->map_x, std::max(nx, ny) * hw * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&p->map_s, ns * hw * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&p->map_y, ny * hw * sizeof(float2)) != hipSuccess) {
+    for (void** q : {(void**)&p->map_field, (void**)&p->map_inten, (void**)&p->map_stats, (void**)&p->map_q,
+                     (void**)&p->map_d4, (void**)&p->map_part, (void**)&p->map_x, (void**)&p->map_s,
+                     (void**)&p->map_y})
+      if (*q) { (void)hipFree(*q); *q = nullptr; }
+    return fail(HBX_ERR_NOMEM, "flip-map workspace");
+  }
+  HBX_HIP(hbx::map_prepare_h(pd, p->map_q, p->map_s, p->map_part, p->map_d4, st));
+  return HBX_OK;
+}
+}  // namespace
+
+int hbx_flip_map(hbx_plan_t p, const uint64_t* mask, const float* target, float* dpsnr, double* base_psnr,
+                 void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!mask || !target || !dpsnr) return fail(HBX_ERR_INVALID, "flip map needs mask, target and dpsnr");
+  if (p->pd.P % 2) return fail(HBX_ERR_INVALID, "flip map needs an even plane count");
+  if (p->max_jobs < p->pd.G) return fail(HBX_ERR_INVALID, "flip map needs max_jobs >= groups");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  rc = ensure_map(p, st);
+  if (rc) return rc;
+  const PlanDev& pd = p->pd;
+  const int G = pd.G;
+  double* stats = p->map_stats;
+  rc = propagate_full(p, mask, target, nullptr, 1, p->map_inten, stats, stats + 3 * G, nullptr,
+                      p->map_field, st);
+  if (rc) return rc;
+  for (int g = 0; g < G; ++g)
+    HBX_HIP(hbx::map_group(pd, g, p->map_field, p->map_inten, target, mask, stats, p->map_q, p->map_d4,
+                           p->map_x, p->map_s, p->map_y, dpsnr, pixel_count(p), p->optics.rel_scale,
+                           p->optics.peak, st));
+  if (base_psnr)
+    HBX_HIP(hipMemcpyAsync(base_psnr, stats + 3 * G, sizeof(double), hipMemcpyDeviceToDevice, st));
   return HBX_OK;
 }
 

@@ -77,6 +77,18 @@ struct EnvParams {
 // field_out (nullable): [env][G*P][N][N] complex field of every propagated plane
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, float2* field_out, hipStream_t st);
+// 2-D FFT of n_planes [N][N] complex planes in a (result in a; b is scratch of
+// the same size).  Unnormalised both ways.
+hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,
+                     hipStream_t st);
+// flip map (hbx_map.hip): h-side spectra q [G][4][N][N] + sum |h|^4 per group,
+// then one group's dPSNR map [P][N][N] into out + g*P*N*N
+hipError_t map_prepare_h(const PlanDev& pd, float2* q, float2* scratch, double* part, double* d4,
+                         hipStream_t st);
+hipError_t map_group(const PlanDev& pd, int g, const float2* field, const float* inten,
+                     const float* target, const uint64_t* mask, const double* stats, const float2* q,
+                     const double* d4, float2* X, float2* S, float2* Y, float* out, double count, int rel,
+                     double peak, hipStream_t st);
 hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                            const float2* field, const float* inten, const float* target,
                            const double* chan_stats, hipStream_t st);

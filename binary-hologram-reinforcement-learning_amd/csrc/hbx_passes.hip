@@ -619,6 +619,81 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
 }
 
 // ---------------------------------------------------------------------------
+// Generic complex 2-D FFT (flip-map correlations): a row pass that writes its
+// result transposed.  in [n][N][N] row-major -> out[n][k][y] = FFT_x in[n][y][x];
+// two applications give the 2-D transform in natural orientation.  Same
+// 32-lane group FFT and LDS tile transpose as k_rowfwd (64-B pieces of each
+// output line, XCD-grouped row blocks).  INV: + sign, no 1/N^2.
+// ---------------------------------------------------------------------------
+template <int R, bool INV>
+__global__ __launch_bounds__(256, 2) void k_fft_rt(const float2* __restrict__ in,
+                                                   float2* __restrict__ out,
+                                                   const float2* __restrict__ tw_glob) {
+  constexpr int N = R * R;
+  constexpr int GPB = 256 / R;
+  constexpr int SCR = GPB * R * (R + 1);
+  static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
+  constexpr int RB = N / GPB;
+  __shared__ float2 tw[N];
+  __shared__ __attribute__((aligned(16))) float2 lds[SCR];
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  int bid = xcd_pair<RB>(blockIdx.x);
+  const int rb = bid % RB;
+  const int plane = bid / RB;
+  const int y0 = rb * GPB;
+  const float2* row = in + ((size_t)plane * N + y0 + grp) * N + t;
+  float2 v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) v[j] = row[R * j];
+  __syncthreads();  // tw visible
+  fft_group<R, INV>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
+  lds_barrier();    // scratch reused as the tile [k][row]
+#pragma unroll
+  for (int k2 = 0; k2 < R; ++k2) lds[tile_pos<R>(t + R * k2, grp)] = v[k2];
+  lds_barrier();
+  float2* base = out + (size_t)plane * N * N;
+  constexpr int CHUNKS = N * GPB / 2;
+#pragma unroll
+  for (int i = 0; i < CHUNKS / 256; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int r2 = (c % (GPB / 2)) * 2;
+    const int line = c / (GPB / 2);
+    const float2 a = lds[tile_pos<R>(line, r2)];
+    const float2 b = lds[tile_pos<R>(line, r2 + 1)];
+    *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
+template <int R>
+static hipError_t launch_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,
+                               hipStream_t st) {
+  constexpr int N = R * R;
+  const unsigned blocks = (unsigned)n_planes * (N / (256 / R));
+  for (int pass = 0; pass < 2; ++pass) {
+    const float2* src = pass == 0 ? a : b;
+    float2* dst = pass == 0 ? b : a;
+    if (inverse)
+      hipLaunchKernelGGL((k_fft_rt<R, true>), dim3(blocks), dim3(256), 0, st, src, dst, pd.tw);
+    else
+      hipLaunchKernelGGL((k_fft_rt<R, false>), dim3(blocks), dim3(256), 0, st, src, dst, pd.tw);
+  }
+  return hipGetLastError();
+}
+
+hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,
+                     hipStream_t st) {
+  if (n_planes <= 0) return hipSuccess;
+  switch (pd.R) {
+    case 32: return launch_fft2d<32>(pd, a, b, n_planes, inverse, st);
+    case 16: return launch_fft2d<16>(pd, a, b, n_planes, inverse, st);
+    case 8: return launch_fft2d<8>(pd, a, b, n_planes, inverse, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launch sequence for one batch of jobs
 // ---------------------------------------------------------------------------
 __global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,

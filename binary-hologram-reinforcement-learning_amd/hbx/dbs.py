@@ -147,3 +147,39 @@ def probe(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips, pre_model
             res.improved_bins[i] = int((sel & improved).sum())
             res.delta_bins[i] = float(np.sum((ps - base)[sel & improved]))
     return res
+
+
+def probe_map(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips=None,
+              pre_model=None, stream=None) -> ProbeResult:
+    """The probe sweep from the all-flip PSNR-change map (hbx_flip_map):
+    every flip of the fixed base at once, then the requested ``flips`` (or all
+    CH*H*W of them) read out of the map.  Same result fields as probe();
+    the pre-model histogram is binned on the device."""
+    dev = plan.device
+    dmap, base_t = plan.flip_map(mask, target, stream=stream)
+    base = float(base_t.item())
+    flat = dmap.reshape(-1)
+    if flips is None:
+        idx = None
+        delta = flat.double()
+    else:
+        idx = torch.as_tensor(np.asarray(flips, np.int64)).to(dev)
+        delta = flat[idx].double()
+    improved = delta > 0
+    res = ProbeResult(base, (delta + base).cpu().numpy(), improved.cpu().numpy())
+    if pre_model is not None:
+        pm = torch.as_tensor(np.asarray(pre_model, np.float32)).to(dev).reshape(-1)
+        vals = (pm if idx is None else pm[idx]).double()
+        edges = torch.as_tensor(OUTPUT_BINS[1:10], dtype=torch.float64, device=dev)
+        bins = torch.bucketize(vals, edges, right=True)
+        bins = torch.where((vals < 0) | (vals > 1.0), torch.full_like(bins, -1), bins)
+        ok = bins >= 0
+        b = bins.clamp(min=0)
+        att = torch.zeros(10, dtype=torch.int64, device=dev).index_add_(0, b[ok], torch.ones_like(b[ok]))
+        sel = ok & improved
+        imp = torch.zeros(10, dtype=torch.int64, device=dev).index_add_(0, b[sel], torch.ones_like(b[sel]))
+        dsum = torch.zeros(10, dtype=torch.float64, device=dev).index_add_(0, b[sel], delta[sel])
+        res.attempted_bins = att.cpu().numpy()
+        res.improved_bins = imp.cpu().numpy()
+        res.delta_bins = dsum.cpu().numpy()
+    return res

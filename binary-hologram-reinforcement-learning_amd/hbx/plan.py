@@ -202,6 +202,22 @@ class Plan:
         _lib.check(self.lib.hbx_psnr(self._h, _ptr(chan_stats), n, _ptr(out), _stream(stream)), "hbx_psnr")
         return out
 
+    def flip_map(self, mask: torch.Tensor, target: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 stream=None):
+        """PSNR change of every single-pixel flip of ONE env against its
+        current state (hbx_flip_map): returns (dpsnr f32 [CH, H, W], base
+        psnr f64 [1]).  dpsnr.flatten()[a] is the change for action a."""
+        c = self.cfg
+        _need(mask, "mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        if out is None:
+            out = torch.empty((c.channels, c.height, c.width), dtype=torch.float32, device=self.device)
+        _need(out, "out", torch.float32, (c.channels, c.height, c.width), self.device)
+        base = torch.empty((1,), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_flip_map(self._h, _ptr(mask), _ptr(target), _ptr(out), _ptr(base),
+                                         _stream(stream)), "hbx_flip_map")
+        return out, base
+
     def eval_flips(self, base_mask: torch.Tensor, target: torch.Tensor, base_stats: torch.Tensor,
                    flips: torch.Tensor, psnr_out: Optional[torch.Tensor] = None,
                    group_stats: Optional[torch.Tensor] = None, stream=None):

@@ -173,6 +173,19 @@ int hbx_eval_flips(hbx_plan_t plan, const uint64_t* base_mask, const float* targ
                    const double* base_chan_stats, const int64_t* flips, int32_t K,
                    double* psnr_out, double* group_stats, void* stream);
 
+/* PSNR change of EVERY single-pixel flip of one env against its current
+ * state, all CH*H*W of them at once (the full probe sweep
+ * DBS_1024_24-128.py:310-373 / range.py:294-335 and env_group.py:90-143's
+ * sampled importance pass, without one propagation per flip):
+ *   dpsnr[c][r][col] = PSNR(state with (c, r, col) toggled) - PSNR(state)
+ * By linearity a flip adds delta * h_g(. - x0) to one plane's field, so the
+ * new (sum I T, sum I^2) are correlations of functions of the fields, the
+ * intensity and the target with functions of the single-pixel field h_g,
+ * evaluated with 2-D FFTs (hbx_map.hip).  mask [CH][H][W/64], target
+ * [G][H][W] (one env), dpsnr [CH][H][W] f32, base_psnr (nullable) f64. */
+int hbx_flip_map(hbx_plan_t plan, const uint64_t* mask, const float* target, float* dpsnr,
+                 double* base_psnr, void* stream);
+
 /* Commit one accepted candidate of hbx_eval_flips into the base env:
  * toggle mask bit `flips[k]`, chan_stats[g] = group_stats[k], prev_psnr =
  * psnr_out[k].  Device-side; `k` is a device int32 (from the host or a

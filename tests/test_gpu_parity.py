@@ -335,3 +335,89 @@ def test_psf_matches_fft_full_size(field_kind):
     assert torch.equal(fft.state.mask, psf.state.mask)
     fft.close()
     psf.close()
+
+
+# ---------------------------------------------------------------------------
+# all-flip PSNR-change map (hbx_flip_map, correlation evaluation)
+# ---------------------------------------------------------------------------
+MAP_TOL = 1e-8   # dB: the map evaluates each flip's increments directly (measured
+                 # <= 1e-9 dB at 64^2 / 256^2 and ~1e-12 dB at 1024^2 against the f64 oracle)
+
+
+def test_flip_map_probe_golden(golden_dir):
+    import hbx
+    from hbx import dbs
+    d = load(golden_dir, "probe_64.npz")
+    cfg = dev_cfg(small_rgb())
+    plan = hbx.Plan(cfg, max_jobs=8)
+    mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
+    res = dbs.probe_map(plan, mask, torch.from_numpy(d["target"]).cuda(), d["flips"], pre_model=d["pre_model"])
+    assert abs(res.base_psnr - float(d["base_psnr"])) <= PSNR_TOL
+    delta = d["psnr"] - d["base_psnr"]
+    err = np.max(np.abs((res.psnr - res.base_psnr) - delta))
+    assert err <= MAP_TOL, err
+    clear = np.abs(delta) > MAP_TOL
+    assert np.array_equal(res.improved[clear], (delta > 0)[clear])
+    assert np.array_equal(res.attempted_bins, d["attempted"])
+    assert np.sum(np.abs(res.improved_bins - d["improved"])) <= np.sum(~clear)
+    assert np.allclose(res.delta_bins, d["delta_sum"], rtol=0, atol=2048 * MAP_TOL)
+
+
+@pytest.mark.parametrize("field", ["amplitude", "phase"])
+def test_flip_map_every_flip_256(field):
+    """Every one of the 524 288 flips of a 256x256x8 mono state vs the oracle
+    on a sample, and vs hbx_eval_flips (brute-force propagation) on another."""
+    import hbx
+    fk = O.FIELD_AMPLITUDE if field == "amplitude" else O.FIELD_PHASE
+    ocfg = O.mono_config(256, field_kind=fk)
+    pre, tgt = O.synthetic_inputs(ocfg, 41)
+    env = O.OracleEnv(ocfg)
+    base = env.reset(pre, tgt)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=256)
+    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    t = torch.from_numpy(tgt).cuda()
+    dmap, b = plan.flip_map(bits, t)
+    assert abs(float(b.item()) - base) <= PSNR_TOL
+    flat = dmap.reshape(-1).cpu().numpy().astype(np.float64)
+    assert np.all(np.isfinite(flat))
+    rng = np.random.default_rng(42)
+    sample = rng.integers(0, ocfg.channels * 256 * 256, 48)
+    want = np.array([env.evaluate_flip(int(a))[0] - base for a in sample])
+    err = np.max(np.abs(flat[sample] - want))
+    assert err <= MAP_TOL, (err, np.max(np.abs(want)))
+    # brute force on the GPU for 256 more
+    s2 = torch.from_numpy(rng.integers(0, ocfg.channels * 256 * 256, 256)).cuda()
+    _, st, _ = plan.propagate(bits[None], t[None])
+    ps, _ = plan.eval_flips(bits, t, st[0].contiguous(), s2)
+    assert np.max(np.abs(flat[s2.cpu().numpy()] - (ps.cpu().numpy() - base))) <= PSNR_TOL
+
+
+def test_flip_map_1024_rgb_vs_eval_flips():
+    """Full size (24 x 1024 x 1024 = 25.2 M flips in one call) against brute-force
+    propagation of 256 random flips plus the corners of every plane."""
+    import hbx
+    ocfg = O.rgb_config(1024)
+    pre, tgt = O.synthetic_inputs(ocfg, 5)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=256)
+    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    t = torch.from_numpy(tgt).cuda()
+    dmap, base = plan.flip_map(bits, t)
+    n = 1024 * 1024
+    corners = [c * n + off for c in range(24) for off in (0, 1023, n - 1024, n - 1)]
+    flips = np.concatenate([np.random.default_rng(6).integers(0, 24 * n, 256), corners]).astype(np.int64)
+    f_t = torch.from_numpy(flips).cuda()
+    _, st, _ = plan.propagate(bits[None], t[None])
+    ps, _ = plan.eval_flips(bits, t, st[0].contiguous(), f_t)
+    got = dmap.reshape(-1)[f_t].double().cpu().numpy()
+    want = ps.cpu().numpy() - float(base.item())
+    err = np.max(np.abs(got - want))
+    assert err <= PSNR_TOL, err
+    assert bool(torch.isfinite(dmap).all())
+    # the map is the more precise of the two (it sums each flip's increment
+    # directly; eval_flips subtracts two full-image PSNRs): f64 oracle check
+    env = O.OracleEnv(ocfg)
+    b0 = env.reset(pre, tgt)
+    few = np.array([0, 5 * n + 77, 13 * n + 512 * 1024 + 3, 24 * n - 1])
+    exact = np.array([env.evaluate_flip(int(a))[0] - b0 for a in few])
+    got = dmap.reshape(-1)[torch.from_numpy(few).cuda()].double().cpu().numpy()
+    assert np.max(np.abs(got - exact)) <= MAP_TOL

@@ -7,7 +7,7 @@ TAG=${1:-run}; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --steps 6 --warmup 2 --psf-steps 20 --cpu-sample 0 --dbs-flips 0 --no-psnr-check $*"
+BENCH="python3 bench.py --steps 6 --warmup 2 --psf-steps 20 --cpu-sample 0 --dbs-flips 0 --no-probe --no-psnr-check $*"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1 || exit 1
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $BENCH > $OUT/fetch.log 2>&1 || exit 2
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $BENCH > $OUT/write.log 2>&1 || exit 3

@@ -8,7 +8,7 @@ LIBS=${*:-$(ls $LIBDIR/libhbx*.so)}
 mkdir -p gpurun_out/variants
 for lib in $LIBS; do
   name=$(basename $lib .so)
-  HBX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-psf --cpu-sample 0 --dbs-flips 0 \
+  HBX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-psf --cpu-sample 0 --dbs-flips 0 --no-probe \
       --no-psnr-check > gpurun_out/variants/$name.json 2> gpurun_out/variants/$name.err || exit 1
   python -c "
 import json; d = json.load(open('gpurun_out/variants/$name.json'))
