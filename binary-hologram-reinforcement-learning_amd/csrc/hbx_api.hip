@@ -51,6 +51,7 @@ struct hbx_plan {
   float* job_inten;       // [max_jobs][N][N]
   int32_t* accept_flag;   // [max_jobs]
   int32_t* err;           // [1]
+  double* delta;          // [max_jobs] psnr change per step (importance rewards)
   // flip-map workspace (lazy, hbx_flip_map)
   float2* map_field = nullptr;   // [CH][N][N]
   float* map_inten = nullptr;    // [G][N][N]
@@ -180,6 +181,7 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "accept_flag");
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
+  if (hipMalloc(&p->delta, (size_t)max_jobs * sizeof(double)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "delta");
   if (hipMalloc(&pd.psf_partial, (size_t)max_jobs * hbx::kPsfBlocks * 2 * sizeof(double)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "psf partials");
   if (hipMalloc(&pd.zero_row, (size_t)N * sizeof(float)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "zero row");
@@ -205,6 +207,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->job_inten) (void)hipFree(p->job_inten);
   if (p->accept_flag) (void)hipFree(p->accept_flag);
   if (p->err) (void)hipFree(p->err);
+  if (p->delta) (void)hipFree(p->delta);
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
@@ -292,6 +295,8 @@ EnvDev env_dev(const hbx_env_buffers_t* e) {
   d.mask = e->mask; d.record = e->record; d.target = e->target; d.chan_stats = e->chan_stats;
   d.init_psnr = e->init_psnr; d.prev_psnr = e->prev_psnr; d.max_psnr_diff = e->max_psnr_diff;
   d.steps = e->steps; d.flip_count = e->flip_count; d.sustained = e->sustained;
+  d.imp_changes = e->imp_changes; d.imp_values = e->imp_values; d.t_psnr_diff = e->t_psnr_diff;
+  d.imp_count = e->imp_count;
   return d;
 }
 
@@ -308,6 +313,9 @@ EnvDev env_offset(const EnvDev& d, size_t e0, int CH, int G, int N) {
   o.steps = d.steps + e0;
   o.flip_count = d.flip_count + e0;
   o.sustained = d.sustained + e0;
+  o.imp_changes = d.imp_changes ? d.imp_changes + e0 * (size_t)d.imp_count : nullptr;
+  o.imp_values = d.imp_values ? d.imp_values + e0 * (size_t)d.imp_count : nullptr;
+  o.t_psnr_diff = d.t_psnr_diff ? d.t_psnr_diff + e0 : nullptr;
   return o;
 }
 
@@ -441,6 +449,10 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
   if (!p->pd.hpsf) return fail(HBX_ERR_INVALID, "incremental mode: call hbx_env_reset with env.field first");
   if (prm->accept_rule != HBX_ACCEPT_ENV && prm->accept_rule != HBX_ACCEPT_DBS)
     return fail(HBX_ERR_INVALID, "accept_rule");
+  if (prm->reward_kind != HBX_REWARD_PSNR && prm->reward_kind != HBX_REWARD_IMPORTANCE)
+    return fail(HBX_ERR_INVALID, "reward_kind");
+  if (prm->reward_kind == HBX_REWARD_IMPORTANCE && (!e->imp_changes || !e->imp_values || e->imp_count <= 0))
+    return fail(HBX_ERR_INVALID, "importance rewards need imp_changes, imp_values and imp_count > 0");
   if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
@@ -451,6 +463,7 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
   ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
   ep.accept_rule = prm->accept_rule;
+  ep.reward_kind = prm->reward_kind;
   const EnvDev base = env_dev(e);
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
@@ -464,7 +477,8 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
                                           reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
                                           accepted ? accepted + b0 : nullptr,
                                           terminated ? terminated + b0 : nullptr,
-                                          truncated ? truncated + b0 : nullptr, p->accept_flag, st));
+                                          truncated ? truncated + b0 : nullptr, p->accept_flag, p->delta,
+                                          st));
     HBX_HIP(hbx::launch_psf_commit(pd, p->jobs, n, ed.mask, fld, inten, p->accept_flag, st));
   }
   return HBX_OK;
@@ -481,6 +495,10 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     return fail(HBX_ERR_INVALID, "env buffers incomplete");
   if (prm->accept_rule != HBX_ACCEPT_ENV && prm->accept_rule != HBX_ACCEPT_DBS)
     return fail(HBX_ERR_INVALID, "accept_rule");
+  if (prm->reward_kind != HBX_REWARD_PSNR && prm->reward_kind != HBX_REWARD_IMPORTANCE)
+    return fail(HBX_ERR_INVALID, "reward_kind");
+  if (prm->reward_kind == HBX_REWARD_IMPORTANCE && (!e->imp_changes || !e->imp_values || e->imp_count <= 0))
+    return fail(HBX_ERR_INVALID, "importance rewards need imp_changes, imp_values and imp_count > 0");
   if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
@@ -496,6 +514,7 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
   ep.accept_rule = prm->accept_rule;
+  ep.reward_kind = prm->reward_kind;
   const EnvDev base = env_dev(e);
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
@@ -508,7 +527,8 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
                                           reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
                                           accepted ? accepted + b0 : nullptr,
                                           terminated ? terminated + b0 : nullptr,
-                                          truncated ? truncated + b0 : nullptr, p->accept_flag, st));
+                                          truncated ? truncated + b0 : nullptr, p->accept_flag, p->delta,
+                                          st));
     if (group_intensity)
       HBX_HIP(hipMemcpyAsync(group_intensity + (size_t)b0 * hw, p->job_inten, (size_t)n * hw * sizeof(float),
                              hipMemcpyDeviceToDevice, st));

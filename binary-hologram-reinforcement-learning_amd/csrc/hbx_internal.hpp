@@ -63,6 +63,10 @@ struct EnvDev {
   int64_t* steps;
   int64_t* flip_count;
   int64_t* sustained;
+  const double* imp_changes;  // [B][imp_count] (importance rewards)
+  const double* imp_values;
+  const double* t_psnr_diff;  // [B] nullable
+  int imp_count;
 };
 
 struct EnvParams {
@@ -72,6 +76,7 @@ struct EnvParams {
   double t_psnr_diff;
   double reward_weight;
   int32_t accept_rule;
+  int32_t reward_kind;  // 0 env.py, 1 env_group.py
 };
 
 // field_out (nullable): [env][G*P][N][N] complex field of every propagated plane
@@ -106,7 +111,7 @@ hipError_t launch_env_step_finalize(const JobDesc* jobs, const double* job_stats
                                     int P, int H, int W, const EnvDev& env, const EnvParams& prm,
                                     double count, int rel, double peak, double* reward, double* psnr,
                                     uint8_t* acc, uint8_t* term, uint8_t* trunc, int32_t* accept_flag,
-                                    hipStream_t st);
+                                    double* delta_scratch, hipStream_t st);
 hipError_t launch_dbs_step_finalize(const JobDesc* jobs, const double* job_stats, int n, int G, int P,
                                     int H, int W, uint64_t* mask, double* chan_stats, double* prev,
                                     double* psnr, uint8_t* acc, int rule, double count, int rel,

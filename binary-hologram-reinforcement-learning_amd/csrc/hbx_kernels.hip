@@ -126,10 +126,11 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
                                     int rel_scale, double peak, double* __restrict__ reward_out,
                                     double* __restrict__ psnr_out, uint8_t* __restrict__ acc_out,
                                     uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                    int32_t* __restrict__ accept_flag) {
+                                    int32_t* __restrict__ accept_flag, double* __restrict__ delta_out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
   const JobDesc jb = jobs[b];
+  if (delta_out) delta_out[b] = NAN;   // no importance lookup for an invalid job
   if (jb.env < 0) {
     if (reward_out) reward_out[b] = 0.0;
     if (psnr_out) psnr_out[b] = env.prev_psnr[b];
@@ -159,7 +160,12 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
   const double psnr_after = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
   const double change = psnr_after - env.prev_psnr[b];   // env.py:184
   const double diff = psnr_after - env.init_psnr[b];     // env.py:185
-  double reward = change * prm.reward_weight;            // env.py:188
+  const bool importance = prm.reward_kind == 1;
+  // env.py:188 / env_group.py:254-255 (the importance term is added by
+  // k_importance_reward from delta_out; here only the bonuses accumulate)
+  double reward = importance ? 0.0 : change * prm.reward_weight;
+  if (delta_out) delta_out[b] = change;
+  const double tpd = env.t_psnr_diff ? env.t_psnr_diff[b] : prm.t_psnr_diff;   // env_group.py:198
   const bool reject = (prm.accept_rule == 0) ? (change < 0.0) : !(change > 0.0);
   bool term = false, trunc = false;
   if (reject) {                                           // env.py:191-196
@@ -172,12 +178,15 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     const double sr = (double)flips / (double)steps;              // env.py:200
     env.prev_psnr[b] = psnr_after;                                // env.py:214
     int64_t sus = env.sustained[b];
-    if (diff >= prm.t_psnr_diff || (psnr_after >= prm.t_psnr && diff < 0.1)) {
+    // env_group.py:292-315: linear in the step count instead of the cubic in sr
+    const double lin = 100.0 + (-200.0 / 1500.0) * (double)(steps - 1000);
+    if (diff >= tpd || (psnr_after >= prm.t_psnr && diff < 0.1)) {
       sus += 1;                                                   // env.py:225
-      if (sus >= prm.t_steps && diff >= prm.t_psnr_diff) reward += success_cubic(sr, 595.2);
+      if (sus >= prm.t_steps && diff >= tpd) reward += importance ? lin : success_cubic(sr, 595.2);
     }
     env.sustained[b] = sus;
-    if (steps >= prm.max_steps) reward += success_cubic(sr, 595.24);   // env.py:249-254
+    if (steps >= prm.max_steps)                                   // env.py:249-254
+      reward += importance ? lin : success_cubic(sr, 595.24);
     term = steps >= prm.max_steps || sus >= prm.t_steps;                // env.py:257
     trunc = steps >= prm.max_steps;                                     // env.py:258
   }
@@ -188,6 +197,41 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
   if (term_out) term_out[b] = term ? 1 : 0;
   if (trunc_out) trunc_out[b] = trunc ? 1 : 0;
   if (accept_flag) accept_flag[b] = reject ? 0 : 1;
+}
+
+// env_group.py:254-255: reward = importance_ranks[argmin |psnr_change_list -
+// change|] (first index on ties, as np.argmin), one block per env
+__global__ void k_importance_reward(const double* __restrict__ delta, const double* __restrict__ changes,
+                                    const double* __restrict__ values, int K, int n,
+                                    double* __restrict__ reward) {
+  const int b = blockIdx.x;
+  if (b >= n) return;
+  const double c = delta[b];
+  if (c != c) return;   // invalid job
+  const double* lst = changes + (size_t)b * K;
+  double best = INFINITY;
+  int bi = K;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) {
+    const double d = fabs(lst[i] - c);
+    if (d < best) { best = d; bi = i; }   // i increases: first index kept on ties
+  }
+  __shared__ double sd[256];
+  __shared__ int si[256];
+  sd[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      const double d2 = sd[threadIdx.x + o];
+      const int i2 = si[threadIdx.x + o];
+      if (d2 < sd[threadIdx.x] || (d2 == sd[threadIdx.x] && i2 < si[threadIdx.x])) {
+        sd[threadIdx.x] = d2;
+        si[threadIdx.x] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && si[0] < K) reward[b] += values[(size_t)b * K + si[0]];
 }
 
 // DBS primitive: accept iff rule, no reward bookkeeping
@@ -337,10 +381,14 @@ hipError_t launch_env_step_finalize(const JobDesc* jobs, const double* job_stats
                                     int P, int H, int W, const EnvDev& env, const EnvParams& prm,
                                     double count, int rel, double peak, double* reward, double* psnr,
                                     uint8_t* acc, uint8_t* term, uint8_t* trunc, int32_t* accept_flag,
-                                    hipStream_t st) {
+                                    double* delta_scratch, hipStream_t st) {
+  const bool imp = prm.reward_kind == 1 && reward && env.imp_changes && env.imp_values && env.imp_count > 0;
   hipLaunchKernelGGL(k_env_step_finalize, dim3((n + 63) / 64), dim3(64), 0, st, jobs, job_stats, n,
                      G, P, H, W, env, prm, count, rel, peak, reward, psnr, acc, term, trunc,
-                     accept_flag);
+                     accept_flag, imp ? delta_scratch : nullptr);
+  if (imp)
+    hipLaunchKernelGGL(k_importance_reward, dim3(n), dim3(256), 0, st, delta_scratch, env.imp_changes,
+                       env.imp_values, env.imp_count, n, reward);
   return hipGetLastError();
 }
 hipError_t launch_dbs_step_finalize(const JobDesc* jobs, const double* job_stats, int n, int G, int P,

@@ -13,13 +13,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 2
+ABI_VERSION = 3
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
 FIELD_AMPLITUDE, FIELD_PHASE = 0, 1
 REL_NONE, REL_LSQ = 0, 1
 ACCEPT_ENV, ACCEPT_DBS = 0, 1
+REWARD_PSNR, REWARD_IMPORTANCE = 0, 1
 MAX_GROUPS = 4
 
 EXPORTED_SYMBOLS = (
@@ -55,6 +56,8 @@ class EnvBuffers(C.Structure):
         ("max_psnr_diff", C.c_void_p), ("steps", C.c_void_p), ("flip_count", C.c_void_p),
         ("sustained", C.c_void_p), ("intensity", C.c_void_p), ("error", C.c_void_p),
         ("field", C.c_void_p),
+        ("imp_changes", C.c_void_p), ("imp_values", C.c_void_p), ("t_psnr_diff", C.c_void_p),
+        ("imp_count", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -62,7 +65,7 @@ class EnvParams(C.Structure):
     _fields_ = [
         ("max_steps", C.c_int64), ("t_psnr", C.c_double), ("t_steps", C.c_int64),
         ("t_psnr_diff", C.c_double), ("reward_weight", C.c_double),
-        ("accept_rule", C.c_int32), ("reserved", C.c_int32),
+        ("accept_rule", C.c_int32), ("reward_kind", C.c_int32),
     ]
 
 

@@ -33,7 +33,7 @@ class EnvState:
     """Device buffers of B environments (env.py:65-81 attributes)."""
 
     def __init__(self, plan: Plan, n_env: int, keep_record: bool = True, keep_pre_model: bool = True,
-                 keep_intensity: bool = True, keep_field: bool = False):
+                 keep_intensity: bool = True, keep_field: bool = False, importance_samples: int = 0):
         c, dev = plan.cfg, plan.device
         self.plan, self.n = plan, n_env
         keep_intensity = keep_intensity or keep_field   # the incremental mode needs both
@@ -58,6 +58,11 @@ class EnvState:
         self.flip_count = torch.zeros(n_env, **i64)
         self.sustained = torch.zeros(n_env, **i64)
         self.error = torch.zeros(1, dtype=torch.int32, device=dev)
+        # env_group.py importance rewards: sampled changes, their importance, T_PSNR_DIFF per env
+        k = int(importance_samples)
+        self.imp_changes = torch.zeros((n_env, k), **f64) if k else None
+        self.imp_values = torch.zeros((n_env, k), **f64) if k else None
+        self.t_psnr_diff = torch.zeros(n_env, **f64) if k else None
         self.bufs = _lib.EnvBuffers()
         p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         b = self.bufs
@@ -66,6 +71,8 @@ class EnvState:
         b.max_psnr_diff, b.steps, b.flip_count = p(self.max_psnr_diff), p(self.steps), p(self.flip_count)
         b.sustained, b.intensity, b.error = p(self.sustained), p(self.intensity), p(self.error)
         b.field = p(self.field)
+        b.imp_changes, b.imp_values, b.t_psnr_diff = p(self.imp_changes), p(self.imp_values), p(self.t_psnr_diff)
+        b.imp_count = k
 
     def check_error(self):
         if int(self.error.item()) != 0:
@@ -81,6 +88,13 @@ class HologramVecEnv:
     (env.py:106-120: the binary state is pre_model >= 0.5), or
     pre_model_source(i) -> the same for env i directly (injected / synthetic).
 
+    reward="psnr" (default) is env.py's RW * change with the cubic bonuses;
+    reward="importance" is env_group.py's: at every reset ``importance_samples``
+    random flips of the fresh state are ranked by PSNR change (read out of the
+    all-flip map, hbx_flip_map), T_PSNR_DIFF becomes (positive sum) / 4 per env,
+    and each step's reward is the importance of the nearest sampled change plus
+    the linear success / max-steps bonuses (hbx/importance.py).
+
     mode="fft" (default) re-propagates the touched colour group every step,
     exactly as the reference does.  mode="psf" is the incremental-field mode
     (include/hbx.h hbx_env_step_psf): same results within fp32 tolerance, one
@@ -94,7 +108,8 @@ class HologramVecEnv:
                  accept_rule: int = _lib.ACCEPT_ENV, max_jobs: Optional[int] = None,
                  obs_keys: Sequence[str] = OBS_KEYS, auto_reset: bool = True,
                  device: Optional[int] = None, pre_model_source: Optional[Callable] = None,
-                 mode: str = "fft", refresh_every: int = 2048):
+                 mode: str = "fft", refresh_every: int = 2048, reward: str = "psnr",
+                 importance_samples: int = 10000, importance_seed: int = 0):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
         if mode not in ("fft", "psf"):
@@ -102,7 +117,13 @@ class HologramVecEnv:
         if mode == "psf" and "recon_image" in obs_keys:
             raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
                              "drop it from obs_keys or use mode='fft'")
+        if reward not in ("psnr", "importance"):
+            raise ValueError(f"reward must be 'psnr' or 'importance', got {reward!r}")
         self.mode = mode
+        self.reward_kind = reward
+        self.importance_samples = int(importance_samples) if reward == "importance" else 0
+        self.importance_seed = int(importance_seed)
+        self._resets = None
         self.refresh_every = int(refresh_every)
         self._since_refresh = 0
         self.cfg = cfg
@@ -117,7 +138,8 @@ class HologramVecEnv:
                               keep_record=True,
                               keep_pre_model="pre_model" in self.obs_keys,
                               keep_intensity="recon_image" in self.obs_keys,
-                              keep_field=(mode == "psf"))
+                              keep_field=(mode == "psf"),
+                              importance_samples=self.importance_samples)
         self.target_source = target_source
         self.pre_model_fn = pre_model_fn
         self.pre_model_source = pre_model_source
@@ -126,6 +148,7 @@ class HologramVecEnv:
         self.params.max_steps, self.params.t_psnr = int(max_steps), float(T_PSNR)
         self.params.t_steps, self.params.t_psnr_diff = int(T_steps), float(T_PSNR_DIFF)
         self.params.reward_weight, self.params.accept_rule = float(reward_weight), int(accept_rule)
+        self.params.reward_kind = _lib.REWARD_IMPORTANCE if reward == "importance" else _lib.REWARD_PSNR
         c = cfg
         self.num_pixels = c.channels * c.height * c.width
         self.action_space = spaces.Discrete(self.num_pixels)           # env.py:50-52
@@ -171,6 +194,25 @@ class HologramVecEnv:
             self._load_env(i)
         idt = torch.tensor(ids, dtype=torch.int32, device=self.device)
         self.plan.env_reset(self.state.bufs, self.num_envs, idt)      # env.py:121-133
+        if self.importance_samples:
+            self._importance_reset(ids)
+
+    def _importance_reset(self, ids):
+        """env_group.py:90-143,198 for the listed envs (see hbx/importance.py)."""
+        from .importance import importance_values
+        st, k = self.state, self.importance_samples
+        if self._resets is None:
+            self._resets = np.zeros(self.num_envs, np.int64)
+        for i in ids:
+            dmap, _ = self.plan.flip_map(st.mask[i], st.target[i])
+            rng = np.random.default_rng([self.importance_seed, i, int(self._resets[i])])
+            self._resets[i] += 1
+            acts = torch.from_numpy(rng.integers(0, self.num_pixels, k)).to(self.device)
+            changes = dmap.reshape(-1)[acts].double()
+            vals, tpd = importance_values(changes.cpu().numpy())
+            st.imp_changes[i].copy_(changes)
+            st.imp_values[i].copy_(torch.from_numpy(vals))
+            st.t_psnr_diff[i] = tpd
 
     def reset(self, seed=None, options=None):
         self.reset_envs(range(self.num_envs))
@@ -280,7 +322,7 @@ class BinaryHologramEnv(spaces.EnvBase):
 
     def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
                  T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, **vec_kwargs):
         super().__init__()
         self.cfg = config or mono_config(256)
         self.target_function = target_function
@@ -291,7 +333,7 @@ class BinaryHologramEnv(spaces.EnvBase):
         self.current_file = None
         self._vec = HologramVecEnv(self.cfg, 1, self._next_target, self._pre_model, max_steps=max_steps,
                                    T_PSNR=T_PSNR, T_steps=T_steps, T_PSNR_DIFF=T_PSNR_DIFF,
-                                   auto_reset=False, device=device)
+                                   auto_reset=False, device=device, **vec_kwargs)
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
         self.num_pixels = self._vec.num_pixels
@@ -346,3 +388,31 @@ class BinaryHologramEnv(spaces.EnvBase):
 
     def close(self):
         self._vec.close()
+
+
+class BinaryHologramEnvGroup(BinaryHologramEnv):
+    """Drop-in for env_group.py's ``BinaryHologramEnv`` (env_group.py:37-320):
+    same constructor and gymnasium contract, importance-rank rewards with the
+    per-episode dynamic T_PSNR_DIFF.  After reset() the sampled
+    ``psnr_change_list``, ``importance_ranks`` and ``T_PSNR_DIFF`` are exposed
+    like the reference's attributes (env_group.py:186-198)."""
+
+    def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 device: Optional[int] = None, importance_samples: int = 10000, importance_seed: int = 0):
+        super().__init__(target_function, trainloader, max_steps=max_steps, T_PSNR=T_PSNR, T_steps=T_steps,
+                         T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device,
+                         reward="importance", importance_samples=importance_samples,
+                         importance_seed=importance_seed)
+        self.psnr_change_list = None
+        self.importance_ranks = None
+
+    def reset(self, seed=None, options=None):
+        obs, info = super().reset(seed=seed, options=options)
+        st = self._vec.state
+        self.psnr_change_list = st.imp_changes[0].cpu().numpy()
+        self.importance_ranks = st.imp_values[0].cpu().numpy()
+        self.T_PSNR_DIFF = float(st.t_psnr_diff[0].item())
+        if self.verbose:
+            print(f"\033[94m[Dynamic Threshold] T_PSNR_DIFF set to: {self.T_PSNR_DIFF:.6f}\033[0m")
+        return obs, info

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 2
+#define HBX_ABI_VERSION 3
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -51,6 +51,11 @@ extern "C" {
 /* accept rule */
 #define HBX_ACCEPT_ENV 0   /* roll back iff delta < 0   (env.py:191)              */
 #define HBX_ACCEPT_DBS 1   /* accept iff psnr > prev    (DBS_1024_24.py:355)      */
+/* reward: env.py:188-254 (RW * change, cubic success / max-steps bonuses)
+ * or env_group.py:250-318 (importance rank of the nearest sampled change,
+ * linear success / max-steps bonuses 100 - (200/1500) (steps - 1000)). */
+#define HBX_REWARD_PSNR 0
+#define HBX_REWARD_IMPORTANCE 1
 
 #define HBX_MAX_GROUPS 4
 
@@ -89,6 +94,13 @@ typedef struct hbx_env_buffers {
   int32_t* error;          /* [1] sticky device error word (nullable)         */
   float* field;            /* [B][G*P][H][W][2] complex64 propagated field of
                               every plane (nullable; incremental-field mode)   */
+  /* env_group.py importance rewards (HBX_REWARD_IMPORTANCE only):            */
+  const double* imp_changes;  /* [B][imp_count] psnr_change_list (env_group.py:90-120) */
+  const double* imp_values;   /* [B][imp_count] importance_ranks (env_group.py:121-143) */
+  const double* t_psnr_diff;  /* [B] per-env T_PSNR_DIFF (dynamic threshold,
+                                 env_group.py:198; nullable -> params value)  */
+  int32_t imp_count;          /* 10000 in the reference                       */
+  int32_t reserved;
 } hbx_env_buffers_t;
 
 /* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
@@ -99,7 +111,7 @@ typedef struct hbx_env_params {
   double t_psnr_diff;      /* 0.1   */
   double reward_weight;    /* 800   */
   int32_t accept_rule;     /* HBX_ACCEPT_ENV */
-  int32_t reserved;
+  int32_t reward_kind;     /* HBX_REWARD_PSNR (env.py) | HBX_REWARD_IMPORTANCE (env_group.py) */
 } hbx_env_params_t;
 
 typedef struct hbx_plan* hbx_plan_t;

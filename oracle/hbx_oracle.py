@@ -361,6 +361,59 @@ class OracleEnv:
         return StepResult(action, psnr_after, reward, True, bool(terminated), bool(truncated))
 
 
+def importance_sample(num_pixels: int, k: int, seed: int, env_index: int = 0, reset_index: int = 0):
+    """The K random flips of an importance reset.  env_group.py:96 draws them
+    with the global np.random.randint; the build seeds them per env and reset
+    (hbx/env.py::_importance_reset uses the same rule)."""
+    return np.random.default_rng([seed, env_index, reset_index]).integers(0, num_pixels, k)
+
+
+def group_linear_bonus(steps: int) -> float:
+    """env_group.py:297-298 / 313-314: 100 + m (steps - 1000), m = -200/1500."""
+    return 100 + (-200.0 / 1500.0) * (steps - 1000)
+
+
+class OracleEnvGroup(OracleEnv):
+    """env_group.py:37-320: importance-rank rewards, dynamic T_PSNR_DIFF."""
+
+    def reset_group(self, pre_model, target, sample_actions):
+        base = self.reset(pre_model, target)
+        ps = probe_sweep(self, sample_actions)                         # env_group.py:90-120
+        self.psnr_change_list = ps - base
+        self.importance_ranks, self.T_PSNR_DIFF = importance_ranks(self.psnr_change_list)  # :121-143,198
+        return base
+
+    def step(self, action: int) -> StepResult:
+        c = self.cfg
+        self.steps += 1                                                # env_group.py:221
+        ch, r, col = (int(v) for v in decode_action(action, c.height, c.width))
+        self.state_record[ch, r, col] += 1                             # env_group.py:231
+        self.flip_count += 1
+        psnr_after, g, ig, st = self.evaluate_flip(action)
+        psnr_change = psnr_after - self.previous_psnr                  # env_group.py:250
+        psnr_diff = psnr_after - self.initial_psnr
+        closest = int(np.argmin(np.abs(np.asarray(self.psnr_change_list) - psnr_change)))
+        reward = float(self.importance_ranks[closest])                 # env_group.py:254-255
+        reject = (psnr_change < 0) if self.accept_rule == 0 else not (psnr_change > 0)
+        if reject:                                                     # env_group.py:258-263
+            self.flip_count -= 1
+            return StepResult(action, psnr_after, reward, False, False, False)
+        self.state[ch, r, col] ^= 1
+        self.intensity[g] = ig
+        self.stats = st
+        self.max_psnr_diff = max(self.max_psnr_diff, psnr_diff)
+        self.previous_psnr = psnr_after                                # env_group.py:281
+        if psnr_diff >= self.T_PSNR_DIFF or (psnr_after >= self.T_PSNR and psnr_diff < 0.1):
+            self.psnr_sustained_steps += 1                             # env_group.py:292
+            if self.psnr_sustained_steps >= self.T_steps and psnr_diff >= self.T_PSNR_DIFF:
+                reward += group_linear_bonus(self.steps)               # env_group.py:294-299
+        if self.steps >= self.max_steps:
+            reward += group_linear_bonus(self.steps)                   # env_group.py:301-315
+        terminated = self.steps >= self.max_steps or self.psnr_sustained_steps >= self.T_steps
+        truncated = self.steps >= self.max_steps
+        return StepResult(action, psnr_after, reward, True, bool(terminated), bool(truncated))
+
+
 # ---------------------------------------------------------------------------
 # DBS drivers
 # ---------------------------------------------------------------------------

@@ -109,6 +109,29 @@ def probe_fixture(n=2048):
             "attempted": att, "improved": imp, "delta_sum": dsum}
 
 
+def env_group_trace(steps=260, k=512, seed=77):
+    """env_group.py importance-reward episode: K sampled flips at reset,
+    nearest-change rewards, dynamic T_PSNR_DIFF, linear bonuses."""
+    cfg = small_rgb_cfg()
+    pre, tgt = O.synthetic_inputs(cfg, 51)
+    env = O.OracleEnvGroup(cfg, max_steps=250, T_PSNR=30.0, T_steps=1)
+    n_pix = cfg.channels * 64 * 64
+    sample = O.importance_sample(n_pix, k, seed)
+    env.reset_group(pre, tgt, sample)
+    acts = np.random.default_rng(52).integers(0, n_pix, steps)
+    rec = [env.step(int(a)) for a in acts]
+    return {"pre_model": pre, "target": tgt, "sample": sample.astype(np.int64),
+            "changes": np.asarray(env.psnr_change_list, np.float64),
+            "importance": np.asarray(env.importance_ranks, np.float64),
+            "t_psnr_diff": np.float64(env.T_PSNR_DIFF), "seed": np.int64(seed),
+            "initial_psnr": np.float64(env.initial_psnr), "actions": acts.astype(np.int64),
+            "psnr": np.array([r.psnr for r in rec]), "reward": np.array([r.reward for r in rec]),
+            "accepted": np.array([r.accepted for r in rec]),
+            "terminated": np.array([r.terminated for r in rec]),
+            "truncated": np.array([r.truncated for r in rec]),
+            "params": np.array([250, 30.0, 1])}
+
+
 def build_all():
     dt = decode_table()
     s, succ, maxs = reward_table()
@@ -120,6 +143,7 @@ def build_all():
         "env_trace_64.npz": env_trace(),
         "dbs_trace_64.npz": dbs_trace(),
         "probe_64.npz": probe_fixture(),
+        "env_group_trace_64.npz": env_group_trace(),
     }
 
 

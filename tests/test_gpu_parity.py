@@ -421,3 +421,52 @@ def test_flip_map_1024_rgb_vs_eval_flips():
     exact = np.array([env.evaluate_flip(int(a))[0] - b0 for a in few])
     got = dmap.reshape(-1)[torch.from_numpy(few).cuda()].double().cpu().numpy()
     assert np.max(np.abs(got - exact)) <= MAP_TOL
+
+
+# ---------------------------------------------------------------------------
+# env_group.py importance rewards
+# ---------------------------------------------------------------------------
+def test_env_group_importance_trace(golden_dir):
+    from hbx.env import HologramVecEnv
+    d = load(golden_dir, "env_group_trace_64.npz")
+    cfg = dev_cfg(small_rgb())
+    k = d["sample"].shape[0]
+    vec = HologramVecEnv(cfg, 1, lambda i: torch.from_numpy(d["target"]).cuda(),
+                         pre_model_source=lambda i: torch.from_numpy(d["pre_model"]).cuda(),
+                         max_steps=250, T_PSNR=30.0, T_steps=1, obs_keys=(), auto_reset=False,
+                         reward="importance", importance_samples=k, importance_seed=int(d["seed"]))
+    vec.reset()
+    st = vec.state
+    changes = st.imp_changes[0].cpu().numpy()
+    assert np.max(np.abs(changes - d["changes"])) <= 1e-8          # read out of the flip map
+    tpd = float(st.t_psnr_diff[0].item())
+    assert abs(tpd - float(d["t_psnr_diff"])) <= k * 1e-8
+    vals = st.imp_values[0].cpu().numpy()
+    clear = np.array([np.sum(np.abs(d["changes"] - c) <= 1e-8) == 1 for c in d["changes"]])
+    assert np.allclose(vals[clear], d["importance"][clear], rtol=0, atol=1e-9)
+    rewards, n_checked = [], 0
+    for t, a in enumerate(d["actions"]):
+        r, ps, acc, term, trunc = vec.step_device(torch.tensor([int(a)], device="cuda"))
+        ps = float(ps.item())
+        assert abs(ps - d["psnr"][t]) <= PSNR_TOL
+        rewards.append(float(r.item()))
+        if abs(float(d["psnr"][t]) - ps) > 1e-7:
+            continue
+        n_checked += 1
+        assert bool(acc.item()) == bool(d["accepted"][t]), t
+        assert bool(term.item()) == bool(d["terminated"][t]), t
+        assert bool(trunc.item()) == bool(d["truncated"][t]), t
+    # reward = importance of the sampled change nearest to the step's change (+ bonus):
+    # the device may pick a neighbour rank when two sampled changes are closer than
+    # its PSNR error, so compare against every candidate within that margin
+    prev = float(d["initial_psnr"])
+    for t in range(len(d["actions"])):
+        c = d["psnr"][t] - prev
+        dist = np.abs(d["changes"] - c)
+        cand = d["importance"][dist <= dist.min() + 2 * 1e-7]
+        bonus = d["reward"][t] - d["importance"][np.argmin(dist)]
+        assert np.min(np.abs(cand + bonus - rewards[t])) <= 1e-6, t
+        if d["accepted"][t]:
+            prev = d["psnr"][t]
+    assert n_checked > 200
+    vec.close()

@@ -214,3 +214,33 @@ def test_golden_dbs_prefix(golden_dir):
     acc, ps, _ = O.dbs_greedy(env, d["order"][:300])
     assert np.array_equal(acc, d["accepted"][:300])
     assert np.allclose(ps, d["psnr"][:300], atol=1e-10)
+
+
+def test_env_group_trace_golden(golden_dir):
+    """The importance-reward oracle (env_group.py) reproduces its committed trace."""
+    import importlib.util, os
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(golden_dir, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    d = np.load(os.path.join(golden_dir, "env_group_trace_64.npz"))
+    got = mg.env_group_trace()
+    for k in ("sample", "changes", "importance", "actions", "accepted", "terminated", "truncated"):
+        assert np.array_equal(got[k], d[k]), k
+    assert np.allclose(got["reward"], d["reward"], rtol=0, atol=1e-12)
+    assert float(got["t_psnr_diff"]) == float(d["t_psnr_diff"])
+
+
+def test_importance_values_match_reference_formula():
+    """hbx/importance.py vs the oracle (env_group.py:121-143,198), incl. ties."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "binary-hologram-reinforcement-learning_amd"))
+    from hbx.importance import importance_values
+    rng = np.random.default_rng(3)
+    ch = rng.normal(0, 1e-3, 10000)
+    ch[5:50] = ch[0]                      # duplicated draws (ties)
+    v, t = importance_values(ch)
+    w, u = O.importance_ranks(ch)
+    assert np.array_equal(v, w) and t == u
+    # the polynomial passes through the reference's six anchor points
+    from hbx.importance import rank_polynomial, STEP_POLY, REWARDS_POLY
+    assert np.allclose(rank_polynomial()(STEP_POLY), REWARDS_POLY, atol=1e-9)
