@@ -14,6 +14,8 @@ probe()   -- DBS_1024_24-128.py:310-373 / range.py:294-335: every flip
 """
 from __future__ import annotations
 
+import io
+import time
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -34,6 +36,9 @@ class GreedyResult:
     accepted_psnr: List[float]
     launches: int
     stopped_early: bool = False
+    accept_times: List[float] = field(default_factory=list)   # seconds since start, per accept
+    last_psnr: Optional[float] = None    # psnr of the last visited candidate (accepted or not)
+    seconds: float = 0.0
 
 
 class KController:
@@ -76,8 +81,10 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     kdev = torch.empty(1, dtype=torch.int32, device=dev)
     ctl = KController(k_min=k_min, k_max=k_max, k0=min(16, k_max))
     pos, launches = 0, 0
-    acc_pos, acc_psnr = [], []
+    acc_pos, acc_psnr, acc_t = [], [], []
     stopped = False
+    last = None
+    t0 = time.perf_counter()
     while pos < total:
         k = min(ctl.k, total - pos)
         flips = order_t[pos:pos + k]
@@ -87,18 +94,106 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         i = first_improving(ps, prev)
         ctl.update(i)
         if i is None:
+            last = float(ps[k - 1])
             pos += k
             continue
+        last = float(ps[i])
         kdev.fill_(i)
         plan.commit_flip(mask, base_stats, prev_dev, flips, psnr_buf, gst_buf, kdev, stream=stream)
         prev = float(ps[i])
         acc_pos.append(pos + i)
         acc_psnr.append(prev)
+        acc_t.append(time.perf_counter() - t0)
         pos += i + 1
         if stop_diff is not None and prev - init >= stop_diff:      # DBS_ratio_0.5.py:366-372
             stopped = True
             break
-    return GreedyResult(init, prev, pos, acc_pos, acc_psnr, launches, stopped)
+    return GreedyResult(init, prev, pos, acc_pos, acc_psnr, launches, stopped, acc_t, last,
+                        time.perf_counter() - t0)
+
+
+def greedy_report(res: GreedyResult, order, pre_model: np.ndarray, height: int, width: int,
+                  file_name: str = "image", print_every: float = 0.1) -> str:
+    """The console report of DBS_1024_24.py:302-470 for a greedy run, in the
+    exact line formats log_py/DBS_psnr_log.py and log_py/com.py parse: a Step
+    block each time the PSNR crosses initial + k * print_every (with the
+    pre-model range statistics accumulated so far), then the final block.
+    Range statistics follow the reference's bookkeeping: the per-bin pixel
+    counts of the whole pre-model, incremented again for every accepted flip."""
+    out = io.StringIO()
+    pm = np.asarray(pre_model, np.float64)
+    order = np.asarray(order, np.int64)
+    bins = np.zeros(10, np.int64)
+    for i in range(10):
+        lo, hi = OUTPUT_BINS[i], OUTPUT_BINS[i + 1]
+        bins[i] = np.logical_and(pm >= lo, pm <= hi if i == 9 else pm < hi).sum()
+    improved = np.zeros(10, np.int64)
+    gains = [[] for _ in range(10)]
+    thresholds = [res.initial_psnr + i * print_every for i in range(1, 101)]
+    hw = height * width
+
+    def coords(a):
+        c = int(a) // hw
+        k = int(a) % hw
+        return c, k // width, k % width
+
+    def range_lines():
+        tot_imp = int(improved.sum())
+        for i in range(10):
+            tc, ic = int(bins[i]), int(improved[i])
+            r_in = ic / tc if tc > 0 else 0
+            r_tot = ic / tot_imp if tot_imp > 0 else 0
+            s_g = sum(gains[i]) if ic > 0 else 0
+            avg = s_g / ic if ic > 0 else 0
+            print(f"Range {OUTPUT_BINS[i]:.1f}-{OUTPUT_BINS[i + 1]:.1f}: "
+                  f"Total Pixels = {tc}, Improved Pixels = {ic}, "
+                  f"Improvement Ratio (in range) = {r_in:.6f}, "
+                  f"Improvement Ratio (to total improved) = {r_tot:.6f}, "
+                  f"Total PSNR Improvement = {s_g:.6f}, "
+                  f"Average PSNR Improvement = {avg:.8f}", file=out)
+
+    print(f"Starting pixel flip optimization for file {file_name}.png with initial PSNR: "
+          f"{res.initial_psnr:.6f}", file=out)
+    prev = res.initial_psnr
+    for n, (p, ps) in enumerate(zip(res.accepted_positions, res.accepted_psnr)):
+        steps, flips = p + 1, n + 1
+        c, r, col = coords(order[p])
+        t = res.accept_times[n] if n < len(res.accept_times) else res.seconds
+        while thresholds and ps >= thresholds[0]:                  # DBS_1024_24.py:366-396
+            thresholds.pop(0)
+            print(f"Step: {steps}"
+                  f"\nPSNR Before: {prev:.6f} | PSNR After: {ps:.6f} | Change: {ps - prev:.6f} | "
+                  f"Diff: {ps - res.initial_psnr:.6f}"
+                  f"\nSuccess Ratio: {flips / steps:.6f} | Flip Count: {flips}"
+                  f"\nFlip Pixel: Channel={c}, Row={r}, Col={col}"
+                  f"\nTime taken for this data: {t:.2f} seconds", file=out)
+            range_lines()
+            print("\n", file=out)
+        v = pm[c, r, col]                                          # DBS_1024_24.py:399-416
+        for i in range(10):
+            lo, hi = OUTPUT_BINS[i], OUTPUT_BINS[i + 1]
+            if (lo <= v <= hi) if i == 9 else (lo <= v < hi):
+                bins[i] += 1
+                improved[i] += 1
+                gains[i].append(ps - prev)
+                break
+        prev = ps
+    steps = max(res.steps, 1)
+    last = res.last_psnr if res.last_psnr is not None else res.final_psnr
+    diff = last - res.initial_psnr
+    c, r, col = coords(order[res.steps - 1]) if res.steps > 0 else (0, 0, 0)
+    print(f"Step: {res.steps}"                                      # DBS_1024_24.py:425-470
+          f"\nPSNR Before: {prev:.6f} | PSNR After: {last:.6f} | Change: {diff:.6f}"
+          f"\nSuccess Ratio: {len(res.accepted_positions) / steps:.6f} | "
+          f"Flip Count: {len(res.accepted_positions)}"
+          f"\nFlip Pixel: Channel={c}, Row={r}, Col={col}"
+          f"\nTime taken for this data: {res.seconds:.2f} seconds", file=out)
+    print(f"{file_name}.png Optimization completed. Final PSNR improvement: {diff:.6f}", file=out)
+    print(f"Time taken for this data: {res.seconds:.2f} seconds\n", file=out)
+    print("Pre-model output range statistics:", file=out)
+    range_lines()
+    print("\n", file=out)
+    return out.getvalue()
 
 
 @dataclass

@@ -109,7 +109,8 @@ class HologramVecEnv:
                  obs_keys: Sequence[str] = OBS_KEYS, auto_reset: bool = True,
                  device: Optional[int] = None, pre_model_source: Optional[Callable] = None,
                  mode: str = "fft", refresh_every: int = 2048, reward: str = "psnr",
-                 importance_samples: int = 10000, importance_seed: int = 0):
+                 importance_samples: int = 10000, importance_seed: int = 0,
+                 action_format: str = "discrete"):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
         if mode not in ("fft", "psf"):
@@ -117,6 +118,9 @@ class HologramVecEnv:
         if mode == "psf" and "recon_image" in obs_keys:
             raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
                              "drop it from obs_keys or use mode='fft'")
+        if action_format not in ("discrete", "multidiscrete"):
+            raise ValueError(f"action_format must be 'discrete' or 'multidiscrete', got {action_format!r}")
+        self.action_format = action_format
         if reward not in ("psnr", "importance"):
             raise ValueError(f"reward must be 'psnr' or 'importance', got {reward!r}")
         self.mode = mode
@@ -151,7 +155,10 @@ class HologramVecEnv:
         self.params.reward_kind = _lib.REWARD_IMPORTANCE if reward == "importance" else _lib.REWARD_PSNR
         c = cfg
         self.num_pixels = c.channels * c.height * c.width
-        self.action_space = spaces.Discrete(self.num_pixels)           # env.py:50-52
+        if action_format == "multidiscrete":                           # env_md.py:54
+            self.action_space = spaces.MultiDiscrete([c.channels, c.height, c.width])
+        else:
+            self.action_space = spaces.Discrete(self.num_pixels)       # env.py:50-52
         self.observation_space = spaces.Dict({                          # env.py:42-48
             "state_record": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
             "state": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
@@ -234,6 +241,14 @@ class HologramVecEnv:
                 or actions.dtype != torch.int64:
             actions = torch.as_tensor(np.asarray(actions, np.int64) if not isinstance(actions, torch.Tensor)
                                       else actions).to(self.device, torch.int64)
+        if self.action_format == "multidiscrete":
+            # env_md.py:159 `channel, row, col = action` -> the flat index the kernels decode;
+            # an out-of-range component maps outside [0, CH*H*W) and raises like env.py
+            a = actions.reshape(self.num_envs, 3)
+            c = self.cfg
+            bad = ((a < 0) | (a >= torch.tensor([c.channels, c.height, c.width], device=self.device))).any(1)
+            actions = torch.where(bad, torch.full_like(a[:, 0], -1),
+                                  (a[:, 0] * c.height + a[:, 1]) * c.width + a[:, 2])
         actions = actions.reshape(self.num_envs).contiguous()
         self._last_actions = actions
         if self.mode == "psf":
@@ -416,3 +431,28 @@ class BinaryHologramEnvGroup(BinaryHologramEnv):
         if self.verbose:
             print(f"\033[94m[Dynamic Threshold] T_PSNR_DIFF set to: {self.T_PSNR_DIFF:.6f}\033[0m")
         return obs, info
+
+
+class BinaryHologramEnvMD(BinaryHologramEnv):
+    """Drop-in for env_md.py's ``BinaryHologramEnv``: the same env with a
+    ``MultiDiscrete([CH, IPS, IPS])`` action space, step((channel, row, col))
+    (env_md.py:54,156-160)."""
+
+    def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 device: Optional[int] = None):
+        super().__init__(target_function, trainloader, max_steps=max_steps, T_PSNR=T_PSNR, T_steps=T_steps,
+                         T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device,
+                         action_format="multidiscrete")
+
+    def step(self, action):
+        a = torch.as_tensor(np.asarray(action, np.int64).reshape(1, 3), device=self._vec.device)
+        reward, psnr, acc, term, trunc = self._vec.step_device(a)
+        self._vec.state.check_error()
+        obs = _to_numpy(self._vec.observe(stepped=True))
+        st = self._vec.state
+        self.steps = int(st.steps[0].item())
+        self.flip_count = int(st.flip_count[0].item())
+        self.psnr_sustained_steps = int(st.sustained[0].item())
+        self.previous_psnr = float(st.prev_psnr[0].item())
+        return obs, float(reward[0].item()), bool(term[0].item()), bool(trunc[0].item()), {}

@@ -470,3 +470,27 @@ def test_env_group_importance_trace(golden_dir):
             prev = d["psnr"][t]
     assert n_checked > 200
     vec.close()
+
+
+def test_multidiscrete_actions_match_discrete(golden_dir):
+    """env_md.py: MultiDiscrete([CH, IPS, IPS]) actions step exactly like the
+    flat Discrete index c*H*W + r*W + col."""
+    from hbx.env import HologramVecEnv
+    d = load(golden_dir, "env_trace_64.npz")
+    cfg = dev_cfg(small_rgb())
+    mk = lambda fmt: HologramVecEnv(cfg, 1, lambda i: torch.from_numpy(d["target"]).cuda(),  # noqa: E731
+                                    pre_model_source=lambda i: torch.from_numpy(d["pre_model"]).cuda(),
+                                    obs_keys=(), auto_reset=False, action_format=fmt)
+    a, b = mk("discrete"), mk("multidiscrete")
+    a.reset(), b.reset()
+    assert tuple(b.action_space.nvec) == (cfg.channels, 64, 64)
+    for act in d["actions"][:60]:
+        c, k = divmod(int(act), 64 * 64)
+        ra = [t.cpu().numpy() for t in a.step_device(torch.tensor([int(act)], device="cuda"))]
+        rb = [t.cpu().numpy() for t in b.step_device(torch.tensor([[c, k // 64, k % 64]], device="cuda"))]
+        for x, y in zip(ra, rb):
+            assert np.array_equal(x, y)
+    b.step_device(torch.tensor([[cfg.channels, 0, 0]], device="cuda"))
+    with pytest.raises(ValueError):
+        b.state.check_error()
+    a.close(), b.close()

@@ -109,3 +109,36 @@ def test_plan_requires_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         hbx.Plan(hbx.mono_config(64))
+
+
+def test_greedy_report_formats():
+    """hbx.dbs.greedy_report prints the DBS_1024_24.py console lines that the
+    log_py parsers (DBS_psnr_log.py step blocks, com.py range lines) read."""
+    import re
+    from hbx.dbs import GreedyResult, greedy_report
+    H = W = 8
+    rng = np.random.default_rng(0)
+    pre = rng.random((2, H, W)).astype(np.float32)
+    order = rng.permutation(2 * H * W)
+    res = GreedyResult(initial_psnr=10.0, final_psnr=10.35, steps=40,
+                       accepted_positions=[2, 9, 17, 30], accepted_psnr=[10.05, 10.12, 10.25, 10.35],
+                       launches=7, accept_times=[0.1, 0.2, 0.3, 0.4], last_psnr=10.3, seconds=0.5)
+    txt = greedy_report(res, order, pre, H, W, file_name="0801")
+    step_re = re.compile(r"Step: (\d+)\s+PSNR Before: [\d.]+\s+\|\s+PSNR After: [\d.]+\s+\|\s+Change: "
+                         r"[\d.e+-]+\s+\|\s+Diff: ([\d.e+-]+)\s+Success Ratio: ([\d.e+-]+)\s+\|\s+"
+                         r"Flip Count: (\d+).*?Time taken for this data: ([\d.]+) seconds", re.DOTALL)
+    steps = [(int(m.group(1)), float(m.group(2)), int(m.group(4))) for m in step_re.finditer(txt)]
+    # thresholds +0.1 (crossed at the 10.12 accept) and +0.2 / +0.3 (10.25 / 10.35)
+    assert steps == [(10, 0.12, 2), (18, 0.25, 3), (31, 0.35, 4)]
+    range_re = re.compile(r"Range (\d\.\d-\d\.\d): Total Pixels = (\d+), Improved Pixels = (\d+), "
+                          r"Improvement Ratio \(in range\) = ([\d\.]+), Improvement Ratio \(to total "
+                          r"improved\) = ([\d\.]+), Total PSNR Improvement = ([\d\.]+), Average PSNR "
+                          r"Improvement = ([\d\.]+)")
+    final = txt.split("Pre-model output range statistics:")[1]
+    rows = range_re.findall(final)
+    assert len(rows) == 10
+    base = np.histogram(pre, bins=np.linspace(0, 1, 11))[0]
+    assert sum(int(r[2]) for r in rows) == 4                       # every accept binned once
+    assert sum(int(r[1]) for r in rows) == int(base.sum()) + 4     # whole pre-model + accepts
+    assert abs(sum(float(r[5]) for r in rows) - 0.35) < 1e-5
+    assert "0801.png Optimization completed. Final PSNR improvement: 0.300000" in txt
