@@ -494,3 +494,27 @@ def test_multidiscrete_actions_match_discrete(golden_dir):
     with pytest.raises(ValueError):
         b.state.check_error()
     a.close(), b.close()
+
+
+def test_premodel_on_gpu_feeds_env_reset():
+    """BinaryNet (PyTorch-ROCm / MIOpen) as the env's pre_model_fn
+    (env.py:109-120): GPU output vs the CPU module, then the reset state's PSNR
+    vs the oracle on the same binarised mask."""
+    from hbx.env import HologramVecEnv
+    from hbx.premodel import premodel_fn, reference_premodel
+    torch.manual_seed(0)
+    m = reference_premodel(num_hologram=8, in_planes=1)
+    tgt = torch.rand(1, 1, 64, 64)
+    want = m(tgt)
+    mg = m.cuda()
+    got = premodel_fn(mg)(tgt.cuda())
+    assert torch.allclose(got.cpu(), want, atol=1e-4)
+    assert premodel_fn(mg, torch.bfloat16)(tgt.cuda()).shape == (1, 8, 64, 64)
+    ocfg = O.mono_config(64)
+    vec = HologramVecEnv(dev_cfg(ocfg), 1, lambda i: tgt[0].cuda(), pre_model_fn=premodel_fn(mg), obs_keys=("pre_model",))
+    obs = vec.reset()
+    pre = obs["pre_model"][0, 0].cpu().numpy()
+    env = O.OracleEnv(ocfg)
+    base = env.reset(pre, tgt[0].numpy())
+    assert abs(float(vec.state.init_psnr[0].item()) - base) <= PSNR_TOL
+    vec.close()

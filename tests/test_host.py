@@ -1,5 +1,6 @@
 """Host-side logic without a GPU: bit packing, spaces, DBS speculation
 bookkeeping, pre-model binning -- each checked against the oracle."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -142,3 +143,43 @@ def test_greedy_report_formats():
     assert sum(int(r[1]) for r in rows) == int(base.sum()) + 4     # whole pre-model + accepts
     assert abs(sum(float(r[5]) for r in rows) - 0.35) < 1e-5
     assert "0801.png Optimization completed. Final PSNR improvement: 0.300000" in txt
+
+
+def test_binarynet_reference_layout_and_checkpoint(tmp_path):
+    """BinaryNet keeps the reference's module names (checkpoint compatibility,
+    DBS_1024_24.py:48-164) and loads a state_dict with weights_only=True."""
+    import torch
+    from hbx.premodel import BinaryNet, load_premodel, reference_premodel
+    m = reference_premodel(num_hologram=24, in_planes=3)
+    names = {k.rsplit(".", 2)[0] for k in m.state_dict()}
+    want = {f"enc{l}_{i}" for l in range(1, 6) for i in (1, 2)} | {f"pool{l}" for l in range(1, 5)} \
+        | {f"dec{l}_{i}" for l in range(1, 5) for i in (1, 2)} | {f"deconv{l}" for l in range(1, 5)} | {"classifier"}
+    assert names == want
+    assert all(k.endswith((".0.weight", ".0.bias")) for k in m.state_dict())   # conv only, no act / BN
+    full = BinaryNet(num_hologram=8, in_planes=1)
+    assert "enc1_1.2.running_mean" in full.state_dict() and "deconv1.1.weight" in full.state_dict()
+    x = torch.rand(1, 3, 32, 32)
+    y = m(x)
+    assert y.shape == (1, 24, 32, 32) and float(y.min()) >= 0 and float(y.max()) <= 1
+    p = tmp_path / "pre.pth"
+    torch.save({"model": m.state_dict()}, p)
+    m2 = load_premodel(str(p), num_hologram=24)
+    assert torch.equal(m2(x), y)
+
+
+def test_target_folder(tmp_path):
+    from PIL import Image
+    from hbx.premodel import TargetFolder
+    rng = np.random.default_rng(0)
+    for name, (h, w) in (("b.png", (40, 60)), ("a.png", (24, 30))):
+        Image.fromarray((rng.random((h, w, 3)) * 255).astype(np.uint8)).save(tmp_path / name)
+    ds = TargetFolder(str(tmp_path), ips=32, train=False, padding=2)
+    assert [os.path.basename(p) for p in ds.target_list] == ["a.png", "b.png"]
+    t, path = ds[1]
+    assert t.shape == (1, 3, 36, 36) and path.endswith("b.png")
+    src = np.asarray(Image.open(tmp_path / "b.png"), np.float32) / 255.0
+    assert np.allclose(t[0, :, 2:-2, 2:-2].numpy(), np.transpose(src[4:36, 14:46], (2, 0, 1)))
+    t2, _ = ds[0]                                   # 24x30 -> shorter side resized to 32
+    assert t2.shape == (1, 3, 36, 36)
+    tr = TargetFolder(str(tmp_path), ips=32, train=True, seed=3)
+    assert tr[1][0].shape == (1, 3, 32, 32)
