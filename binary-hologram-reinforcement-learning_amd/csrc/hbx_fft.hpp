@@ -14,6 +14,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 namespace hbx {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -69,7 +72,140 @@ __device__ __forceinline__ float c32(int k) {
 }
 __device__ __forceinline__ float s32(int k) { return c32(k - 8); }  // sin(x) = cos(x - pi/2)
 
-// Multiply d by W_M^k = exp(-+ 2 pi i k / M), M | 32, k compile-time after unrolling.
+__host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n / 2); }
+__host__ __device__ constexpr int bitrev(int x, int bits) {
+  int r = 0;
+  for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1) << (bits - 1 - i);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Packed-f32 complex arithmetic (gfx950 VOP3P: one v_pk_* instruction works on
+// both halves of a 64-bit register pair, at the issue cost of one f32 op).
+// op_sel / op_sel_hi pick the source half feeding the low / high result and
+// neg_lo / neg_hi negate it, so the swaps and sign flips of the +-i twiddles
+// and of a complex product cost nothing extra:
+//   a * w       = v_pk_mul (a, w.xx) ; v_pk_fma(-a.y|a.x, w.yy, .)   2 instr.
+//   (a - b)(-i) = (a.y - b.y, b.x - a.x)                           1 instr.
+// The asm statements are not volatile: the compiler schedules them freely.
+// ---------------------------------------------------------------------------
+typedef float pk2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pk2 to_pk(float2 a) { return (pk2){a.x, a.y}; }
+__device__ __forceinline__ float2 from_pk(pk2 a) { return make_float2(a.x, a.y); }
+
+// a * w (w in VGPRs)
+__device__ __forceinline__ pk2 pk_cmul(pk2 a, pk2 w) {
+  pk2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+// a * conj(w)
+__device__ __forceinline__ pk2 pk_cmulc(pk2 a, pk2 w) {
+  pk2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=v"(r) : "v"(a), "v"(w), "v"(t));
+  return r;
+}
+// a * (C + iS) where C / S are one half of the register pair P, possibly
+// swapped (SW) and negated (N1 for C, N2 for S) -- all folded into op_sel /
+// neg modifiers, so the 4 first-octant pairs P_r = (cos, sin)(2 pi r / 32),
+// r = 1..4, serve every compile-time twiddle of a 32-point DFT
+template <bool SW, bool N1, bool N2>
+__device__ __forceinline__ pk2 pk_cmul_sel(pk2 a, pk2 P) {
+  pk2 t, r;
+  if constexpr (!SW && !N1) asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(P));
+  if constexpr (!SW && N1) asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(P));
+  if constexpr (SW && !N1) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(t) : "v"(a), "v"(P));
+  if constexpr (SW && N1) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(P));
+  if constexpr (!SW && !N2)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(P), "v"(t));
+  if constexpr (!SW && N2)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(P), "v"(t));
+  if constexpr (SW && !N2)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(P), "v"(t));
+  if constexpr (SW && N2)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(P), "v"(t));
+  return r;
+}
+
+// first-octant pair P_r, r = 1..4
+__device__ __forceinline__ pk2 octant_pair(int r) { return (pk2){c32(r), s32(r)}; }
+
+// (a - b) * (-i) = (a.y - b.y, b.x - a.x)
+__device__ __forceinline__ pk2 pk_sub_mul_mi(pk2 a, pk2 b) {
+  pk2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]"
+      : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// (a - b) * (+i) = (b.y - a.y, a.x - b.x)
+__device__ __forceinline__ pk2 pk_sub_mul_pi(pk2 a, pk2 b) {
+  pk2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]"
+      : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// (a - b) * W_M^k (forward) or W_M^-k (INV), k / M compile-time after unrolling
+template <bool INV, int K32>
+__device__ __forceinline__ pk2 pk_sub_twiddle_k(pk2 a, pk2 b) {
+  constexpr int k32 = K32 & 31;   // exponent in units of 2pi/32
+  if constexpr (k32 == 0) return a - b;
+  else if constexpr (k32 == 16) return b - a;
+  else if constexpr (k32 == 8) return INV ? pk_sub_mul_pi(a, b) : pk_sub_mul_mi(a, b);
+  else if constexpr (k32 == 24) return INV ? pk_sub_mul_mi(a, b) : pk_sub_mul_pi(a, b);
+  else {
+    // theta = 2 pi (8 q + r) / 32: (cos, sin) theta from P_r (r <= 4) or swap(P_8-r),
+    // rotated by quadrant q; forward twiddles use -sin
+    constexpr int q = k32 / 8, r = k32 % 8;
+    constexpr bool swA = r > 4;
+    constexpr bool sw = swA != (q % 2 == 1);
+    constexpr bool n1 = (q == 1 || q == 2);
+    constexpr bool n2 = (q == 2 || q == 3) != !INV;
+    return pk_cmul_sel<sw, n1, n2>(a - b, octant_pair(swA ? 8 - r : r));
+  }
+}
+
+template <int R, bool INV, int SPAN, int K>
+__device__ __forceinline__ void dft_stage_bfly(pk2 (&w)[R], int start) {
+  const pk2 a = w[start + K], b = w[start + K + SPAN];
+  w[start + K] = a + b;
+  w[start + K + SPAN] = pk_sub_twiddle_k<INV, K * (32 / (2 * SPAN))>(a, b);
+}
+
+template <int R, bool INV, int SPAN, int... Ks>
+__device__ __forceinline__ void dft_stage(pk2 (&w)[R], std::integer_sequence<int, Ks...>) {
+#pragma unroll
+  for (int start = 0; start < R; start += 2 * SPAN) (dft_stage_bfly<R, INV, SPAN, Ks>(w, start), ...);
+}
+
+template <int R, bool INV, int SPAN>
+__device__ __forceinline__ void dft_stages(pk2 (&w)[R]) {
+  dft_stage<R, INV, SPAN>(w, std::make_integer_sequence<int, SPAN>{});
+  if constexpr (SPAN > 1) dft_stages<R, INV, SPAN / 2>(w);
+}
+
+// In-register R-point DFT (R in {4, 8, 16, 32}), radix-2 DIF, natural-order out.
+// forward: X[k] = sum_n x[n] exp(-2 pi i n k / R); inverse: + sign, no scaling.
+// Packed f32: R/2 log2 R butterflies of one v_pk_add + one packed (sub x twiddle)
+// (1 instruction for 1, -1, +-i; 3 otherwise) -- half the VALU of scalar f32.
+template <int R, bool INV>
+__device__ __forceinline__ void dft_reg(pk2 (&w)[R]) {
+  dft_stages<R, INV, R / 2>(w);
+  // DIF leaves X[k] at position bitrev(k): permute (register renaming only)
+  pk2 tmp[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) tmp[k] = w[bitrev(k, ilog2c(R))];
+#pragma unroll
+  for (int k = 0; k < R; ++k) w[k] = tmp[k];
+}
+
+// scalar-f32 variant (lower register pressure: the column pass keeps two
+// lines in registers and spills with the packed one)
 template <bool INV>
 __device__ __forceinline__ float2 twiddle_const(float2 d, int k, int M) {
   const int k32 = (k * (32 / M)) & 31;  // exponent in units of 2pi/32
@@ -78,26 +214,12 @@ __device__ __forceinline__ float2 twiddle_const(float2 d, int k, int M) {
   if (k32 == 16) return make_float2(-d.x, -d.y);
   if (k32 == 24) return INV ? make_float2(d.y, -d.x) : make_float2(-d.y, d.x);
   const float c = c32(k32), s = s32(k32);
-  if (k32 == 4 || k32 == 12 || k32 == 20 || k32 == 28) {
-    // |c| == |s| == sqrt(1/2): 2 mul + 2 add
-    const float ws = INV ? s : -s;
-    return make_float2(c * d.x - ws * d.y, c * d.y + ws * d.x);
-  }
   const float ws = INV ? s : -s;
   return make_float2(fmaf(c, d.x, -ws * d.y), fmaf(c, d.y, ws * d.x));
 }
 
-__host__ __device__ constexpr int ilog2c(int n) { return n <= 1 ? 0 : 1 + ilog2c(n / 2); }
-__host__ __device__ constexpr int bitrev(int x, int bits) {
-  int r = 0;
-  for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1) << (bits - 1 - i);
-  return r;
-}
-
-// In-register R-point DFT (R in {4, 8, 16, 32}), radix-2 DIF, natural-order out.
-// forward: X[k] = sum_n x[n] exp(-2 pi i n k / R); inverse: + sign, no scaling.
 template <int R, bool INV>
-__device__ __forceinline__ void dft_reg(float2 (&v)[R]) {
+__device__ __forceinline__ void dft_reg_scalar(float2 (&v)[R]) {
 #pragma unroll
   for (int span = R / 2; span >= 1; span >>= 1) {
 #pragma unroll
@@ -110,12 +232,21 @@ __device__ __forceinline__ void dft_reg(float2 (&v)[R]) {
       }
     }
   }
-  // DIF leaves X[k] at position bitrev(k): permute (register renaming only)
   float2 tmp[R];
 #pragma unroll
   for (int k = 0; k < R; ++k) tmp[k] = v[bitrev(k, ilog2c(R))];
 #pragma unroll
   for (int k = 0; k < R; ++k) v[k] = tmp[k];
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dft_reg(float2 (&v)[R]) {
+  pk2 w[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) w[k] = to_pk(v[k]);
+  dft_reg<R, INV>(w);
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = from_pk(w[k]);
 }
 
 // Wave-level ordering of LDS traffic between lanes of one wavefront.
@@ -151,29 +282,50 @@ struct ColumnScratch {
 };
 
 // Full N = R*R point FFT by R lanes.  v[j] = x[t + R j] in, v[k2] = X[t + R k2] out.
-// tw: LDS table [k1][t] = W_N^{t k1} (forward sign).
-template <int R, bool INV, class Scratch>
-__device__ __forceinline__ void fft_group(float2 (&v)[R], int t, const Scratch& sc, const float2* tw) {
+// tw: LDS table [k1][t] = W_N^{t k1} (forward sign).  Element type float2 or
+// pk2 (pk2 arrays keep the whole FFT in packed register pairs, no copies).
+template <class T>
+__device__ __forceinline__ pk2 ld_pk(const T& a) {
+  if constexpr (std::is_same<T, pk2>::value) return a; else return to_pk(a);
+}
+template <class T>
+__device__ __forceinline__ T st_pk(pk2 a) {
+  if constexpr (std::is_same<T, pk2>::value) return a; else return from_pk(a);
+}
+
+template <int R, bool INV, bool SCALAR = false, class Scratch, class T>
+__device__ __forceinline__ void fft_group(T (&v)[R], int t, const Scratch& sc, const float2* tw) {
   // keep the twiddle loads local to each FFT: without this barrier the
   // compiler CSEs / hoists them across calls and pins 2R VGPRs for good
   asm volatile("" ::: "memory");
 #ifdef HBX_NO_FFT  // access-pattern ceiling experiments only (tools/): data moves, no arithmetic
   return;
 #endif
-  dft_reg<R, INV>(v);
+  if constexpr (SCALAR) {
+    static_assert(std::is_same<T, float2>::value, "scalar FFT works on float2");
+    dft_reg_scalar<R, INV>(v);
 #pragma unroll
-  for (int k1 = 1; k1 < R; ++k1) {
-    const float2 w = tw[k1 * R + t];
-    v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    for (int k1 = 1; k1 < R; ++k1) {
+      const float2 w = tw[k1 * R + t];
+      v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    }
+  } else {
+    dft_reg<R, INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) {
+      const pk2 w = to_pk(tw[k1 * R + t]);
+      v[k1] = st_pk<T>(INV ? pk_cmulc(ld_pk(v[k1]), w) : pk_cmul(ld_pk(v[k1]), w));
+    }
   }
   wave_sync();  // previous users of the scratch are done
 #pragma unroll
-  for (int k1 = 0; k1 < R; ++k1) *sc.at(t, k1) = v[k1];
+  for (int k1 = 0; k1 < R; ++k1) *reinterpret_cast<T*>(sc.at(t, k1)) = v[k1];
   wave_sync();
 #pragma unroll
-  for (int tt = 0; tt < R; ++tt) v[tt] = *sc.at(tt, t);
+  for (int tt = 0; tt < R; ++tt) v[tt] = *reinterpret_cast<const T*>(sc.at(tt, t));
   wave_sync();
-  dft_reg<R, INV>(v);
+  if constexpr (SCALAR) dft_reg_scalar<R, INV>(v);
+  else dft_reg<R, INV>(v);
 }
 
 // Value of conj(X[N - k]) for k = t + R*k2, fetched from the lane group that

@@ -298,7 +298,8 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 // two-role k_col), one A read, one H read, and no cross-group traffic: every
 // LDS hand-off stays inside the group's own scratch (wave_sync only).  The
 // next line's loads go into v as soon as line kx is stored and fly under the
-// second inverse FFT.
+// second inverse FFT.  Scalar-f32 FFTs here: with two lines in registers the
+// packed variant (hbx_fft.hpp) spills.
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
 
@@ -343,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   for (int it = 0; it < ITER; ++it) {
     const int kx = kx0 + it * GPB;
     const bool dc = (kx == 0);
-    fft_group<R, false>(v, t, sc, tw);
+    fft_group<R, false, true>(v, t, sc, tw);
     // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
     // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
     // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
         m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), hnyq[R * k2]);
       }
     }
-    fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
+    fft_group<R, true, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
     {
       float2* out = bout + (size_t)kx * N;
 #pragma unroll
@@ -389,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #pragma unroll
       for (int jj = 0; jj < R; ++jj) v[jj] = in[R * jj];
     }
-    fft_group<R, true>(m, t, sc, tw);
+    fft_group<R, true, true>(m, t, sc, tw);
     {
       float2* out = bout + (size_t)(dc ? N / 2 : N - kx) * N;
 #pragma unroll
@@ -568,17 +569,17 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
       }
     }
     lds_barrier();
-    float2 v[R];
+    pk2 v[R];
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = tile[tile_pos<R>(t + R * jj, grp)];
+    for (int jj = 0; jj < R; ++jj) v[jj] = to_pk(tile[tile_pos<R>(t + R * jj, grp)]);
     lds_barrier();  // tile consumed: reuse it as transpose scratch
     fft_group<R, true>(v, t, PaddedScratch<R>{tile + grp * R * (R + 1)}, tw);
 #pragma unroll
-    for (int k = 0; k < R; ++k) acc[k] += norm2(v[k]);
+    for (int k = 0; k < R; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
     if (field_out) {  // exact field of this plane (incremental mode init / refresh)
       float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * N + y) * N;
 #pragma unroll
-      for (int k = 0; k < R; ++k) frow[t + R * k] = v[k];
+      for (int k = 0; k < R; ++k) frow[t + R * k] = from_pk(v[k]);
     }
   }
 
