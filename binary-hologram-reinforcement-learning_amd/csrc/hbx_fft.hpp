@@ -331,14 +331,14 @@ __device__ __forceinline__ void fft_group(T (&v)[R], int t, const Scratch& sc, c
 // Value of conj(X[N - k]) for k = t + R*k2, fetched from the lane group that
 // holds it (lane (R - t) mod R, register R-1-k2; lane 0 keeps its own
 // register (R - k2) mod R).  `lane_base` is the first lane of the group.
-template <int R>
-__device__ __forceinline__ float2 mirror_conj(const float2 (&v)[R], int k2, int t, int lane_base) {
+template <int R, class T>
+__device__ __forceinline__ float2 mirror_conj(const T (&v)[R], int k2, int t, int lane_base) {
   const int src = lane_base + ((R - t) & (R - 1));
-  const float2 other = v[R - 1 - k2];
+  const float2 other = make_float2(v[R - 1 - k2].x, v[R - 1 - k2].y);
   float2 p;
   p.x = __shfl(other.x, src, 64);
   p.y = __shfl(other.y, src, 64);
-  const float2 own = v[(R - k2) & (R - 1)];
+  const float2 own = make_float2(v[(R - k2) & (R - 1)].x, v[(R - k2) & (R - 1)].y);
   const float2 z = (t == 0) ? own : p;
   return conjf2(z);
 }

@@ -120,13 +120,12 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ j
       }
     }
   }
-  float2 v[R];
+  pk2 v[R];
 #pragma unroll
   for (int jj = 0; jj < R; ++jj) {
     const int w = (R * jj) >> 5;
     const int sh = ((R * jj) & 31) + t;
-    v[jj].x = fmaf(vb, (float)((wa[w] >> sh) & 1u), va);
-    v[jj].y = fmaf(vb, (float)((wb[w] >> sh) & 1u), va);
+    v[jj] = (pk2){fmaf(vb, (float)((wa[w] >> sh) & 1u), va), fmaf(vb, (float)((wb[w] >> sh) & 1u), va)};
   }
   __syncthreads();  // tw visible
   fft_group<R, false>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
@@ -134,10 +133,10 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ j
 
   // Hermitian split -> tile[plane][kx][row]
   float2* tile = lds;
-  const float2 zny = v[R / 2];  // Z[N/2] on lane 0
+  const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0
 #pragma unroll
   for (int k2 = 0; k2 < R / 2; ++k2) {
-    const float2 z = v[k2];
+    const float2 z = from_pk(v[k2]);
     const float2 m = mirror_conj<R>(v, k2, t, lane_base);
     float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
     float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
