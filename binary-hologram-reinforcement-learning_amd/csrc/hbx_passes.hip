@@ -33,13 +33,29 @@ namespace hbx {
 // then addresses base_t + j*R*GPB (immediate offsets, no per-j address VGPRs),
 // ds_read_b64 is conflict-free and ds_write_b64 at most 2-way (checked
 // exhaustively for R = 8, 16, 32).
-template <int R>
+template <int R, int GPB = 256 / R>
 __device__ __forceinline__ int tile_pos(int line, int r) {
-  constexpr int GPB = 256 / R;
-  constexpr int SR = ilog2c(32 / GPB);
-  constexpr int SL = ilog2c(GPB / 8);
-  return line * GPB + (r ^ ((((line & (R - 1)) >> SR) << SL) & (GPB - 1)));
+  if constexpr (GPB == 16) {
+    // 16 rows (512-thread blocks, N = 1024): swizzle (line mod 16) ^ bit 4 of
+    // line -- conflict-free for the lane-row reads / writes and the 16-B chunk
+    // writes; the chunk reads of k_rowfwd stay 2-way (checked exhaustively)
+    return line * GPB + (r ^ (((line & 15) ^ ((line >> 4) & 1)) & (GPB - 1)));
+  } else {
+    constexpr int SR = ilog2c(32 / GPB);
+    constexpr int SL = ilog2c(GPB / 8);
+    return line * GPB + (r ^ ((((line & (R - 1)) >> SR) << SL) & (GPB - 1)));
+  }
 }
+
+// Threads per block of the row passes at N = 1024.  -DHBX_ROW_NT=512 gives 16
+// rows per block (128-B pieces of every intermediate line, conflict-free
+// swizzle above) but only one 143-KB block per CU, whose barriers then stall
+// the whole CU: measured k_rowfwd 1.17 -> 1.54 ms, k_rowinv 2.01 -> 2.62 ms.
+#ifndef HBX_ROW_NT
+#define HBX_ROW_NT 256
+#endif
+template <int R>
+constexpr int kRowNT = (R == 32) ? HBX_ROW_NT : 256;
 
 // Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
 // the 8 XCDs; placement is a speed hint only, never relied on for
@@ -63,21 +79,21 @@ __device__ __forceinline__ int xcd_pair(int bid) {
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ jobs,
+template <int R, int NT>
+__global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
                                                    const uint32_t* __restrict__ mask,
                                                    float2* __restrict__ ws_a,
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int CH, float va, float vb) {
   constexpr int N = R * R;
-  constexpr int GPB = 256 / R;          // rows per block
+  constexpr int GPB = NT / R;          // rows per block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
   constexpr int SCR = GPB * R * (R + 1);
   static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
   __shared__ float2 tw[N];
   __shared__ __attribute__((aligned(16))) float2 lds[SCR];
 
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+  for (int i = threadIdx.x; i < N; i += NT) tw[i] = tw_glob[i];
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
@@ -145,21 +161,21 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd(const JobDesc* __restrict__ j
       fb = make_float2(z.y, zny.y);
     }
     const int kx = t + R * k2;
-    tile[tile_pos<R>(kx, grp)] = fa;
-    tile[tile_pos<R>(N / 2 + kx, grp)] = fb;
+    tile[tile_pos<R, GPB>(kx, grp)] = fa;
+    tile[tile_pos<R, GPB>(N / 2 + kx, grp)] = fb;
   }
   lds_barrier();
   // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
   float2* base = ws_a + ((size_t)j * P + pa) * (N / 2) * N;
   constexpr int CHUNKS = N * GPB / 2;
-  static_assert(CHUNKS % 256 == 0, "chunking");
+  static_assert(CHUNKS % NT == 0, "chunking");
 #pragma unroll
-  for (int i = 0; i < CHUNKS / 256; ++i) {
-    const int c = threadIdx.x + 256 * i;
+  for (int i = 0; i < CHUNKS / NT; ++i) {
+    const int c = threadIdx.x + NT * i;
     const int r2 = (c % (GPB / 2)) * 2;
     const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
-    const float2 a = tile[tile_pos<R>(line, r2)];
-    const float2 b = tile[tile_pos<R>(line, r2 + 1)];
+    const float2 a = tile[tile_pos<R, GPB>(line, r2)];
+    const float2 b = tile[tile_pos<R, GPB>(line, r2 + 1)];
     *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
   }
 }
@@ -299,6 +315,22 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 // next line's loads go into v as soon as line kx is stored and fly under the
 // second inverse FFT.  Scalar-f32 FFTs here: with two lines in registers the
 // packed variant (hbx_fft.hpp) spills.
+#ifndef HBX_COL2_SCALAR
+#define HBX_COL2_SCALAR true
+#endif
+#if HBX_COL2_SCALAR
+#define COL2_T float2
+#define COL2_LD(x) (x)
+#define COL2_ST(x) (x)
+#define COL2_CMUL(a, b) cmul((a), (b))
+#define COL2_CMULC(a, b) cmulc((a), (b))
+#else
+#define COL2_T pk2
+#define COL2_LD(x) to_pk(x)
+#define COL2_ST(x) from_pk(x)
+#define COL2_CMUL(a, b) pk_cmul((a), to_pk(b))
+#define COL2_CMULC(a, b) from_pk(pk_cmulc((a), to_pk(b)))
+#endif
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
 
@@ -334,16 +366,16 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
   const int kx0 = lb * (GPB * ITER) + grp;
 
-  float2 v[R];
+  COL2_T v[R];
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) v[jj] = ain[(size_t)kx0 * N + R * jj];
+  for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(ain[(size_t)kx0 * N + R * jj]);
   lds_barrier();  // tw visible (the line loads stay in flight)
 
 #pragma unroll 1
   for (int it = 0; it < ITER; ++it) {
     const int kx = kx0 + it * GPB;
     const bool dc = (kx == 0);
-    fft_group<R, false, true>(v, t, sc, tw);
+    fft_group<R, false, HBX_COL2_SCALAR>(v, t, sc, tw);
     // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
     // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
     // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
@@ -353,47 +385,53 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     wave_sync();
     if (!dc) {
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) {
-        const float2 h = hrow[R * k2];
-        const float2 w = cmulc(v[k2], h);
-        *sc.at(t, k2) = w;
-        if (k2 == 0) *sc.at(t, R) = w;
-        v[k2] = cmul(v[k2], h);
+      for (int c8 = 0; c8 < R; c8 += 8) {   // H in batches of 8 loads
+        float2 hb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[i] = hrow[R * (c8 + i)];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k2 = c8 + i;
+          const float2 w = COL2_CMULC(v[k2], hb[i]);
+          *sc.at(t, k2) = w;
+          if (k2 == 0) *sc.at(t, R) = w;
+          v[k2] = COL2_CMUL(v[k2], hb[i]);
+        }
       }
     } else {  // kx = 0: one group of the whole plane; plain Z through the scratch
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
-      *sc.at(t, R) = v[0];
+      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = COL2_ST(v[k2]);
+      *sc.at(t, R) = COL2_ST(v[0]);
     }
     wave_sync();
-    float2 m[R];
+    COL2_T m[R];
 #pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) m[k2] = conjf2(mrow[-k2]);
+    for (int k2 = 0; k2 < R; ++k2) m[k2] = COL2_LD(conjf2(mrow[-k2]));
     if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
       const float2* hnyq = hg + (size_t)(N / 2) * N;
 #pragma unroll
       for (int k2 = 0; k2 < R; ++k2) {
-        const float2 z = v[k2], mm = m[k2];
-        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), hrow[R * k2]);
-        m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), hnyq[R * k2]);
+        const float2 z = COL2_ST(v[k2]), mm = COL2_ST(m[k2]);
+        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), hrow[R * k2]));
+        m[k2] = COL2_LD(cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), hnyq[R * k2]));
       }
     }
-    fft_group<R, true, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
+    fft_group<R, true, HBX_COL2_SCALAR>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
     {
       float2* out = bout + (size_t)kx * N;
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = v[k2];
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = COL2_ST(v[k2]);
     }
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
       const float2* in = ain + (size_t)(kx + GPB) * N;
 #pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = in[R * jj];
+      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(in[R * jj]);
     }
-    fft_group<R, true, true>(m, t, sc, tw);
+    fft_group<R, true, HBX_COL2_SCALAR>(m, t, sc, tw);
     {
       float2* out = bout + (size_t)(dc ? N / 2 : N - kx) * N;
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = m[k2];
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = COL2_ST(m[k2]);
     }
   }
 }
@@ -498,8 +536,8 @@ __global__ __launch_bounds__(256, 3) void k_col_w(const JobDesc* __restrict__ jo
 // ---------------------------------------------------------------------------
 // Pass 3
 // ---------------------------------------------------------------------------
-template <int R>
-__global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ jobs,
+template <int R, int NT>
+__global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restrict__ jobs,
                                                    const float2* __restrict__ ws_b,
                                                    const float* __restrict__ target,
                                                    const float2* __restrict__ tw_glob, int P,
@@ -508,17 +546,17 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
                                                    float2* __restrict__ field_out,
                                                    size_t tmask) {
   constexpr int N = R * R;
-  constexpr int GPB = 256 / R;          // rows per block
+  constexpr int GPB = NT / R;          // rows per block
   constexpr int RB = N / GPB;
   constexpr int CH16 = N * GPB / 2;     // 16-B chunks per plane tile
-  constexpr int PER = CH16 / 256;
-  static_assert(CH16 % 256 == 0, "chunking");
+  constexpr int PER = CH16 / NT;
+  static_assert(CH16 % NT == 0, "chunking");
   constexpr int SCR = GPB * R * (R + 1);   // padded transpose scratch reuses the tile
   __shared__ float2 tw[N];
   __shared__ __attribute__((aligned(16))) float2 tile[SCR > N * GPB ? SCR : N * GPB];
   __shared__ double red[GPB][3];
 
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+  for (int i = threadIdx.x; i < N; i += NT) tw[i] = tw_glob[i];
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
@@ -540,7 +578,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
   float4 pre[PER];   // this thread's share of a plane tile, one plane ahead
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + 256 * i;
+    const int c = threadIdx.x + NT * i;
     const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
     pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * N + y0 + r2);
   }
@@ -553,16 +591,16 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
     lds_barrier();  // previous plane's scratch use is over (also publishes tw)
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + 256 * i;
+      const int c = threadIdx.x + NT * i;
       const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-      tile[tile_pos<R>(line, r2)] = make_float2(pre[i].x, pre[i].y);
-      tile[tile_pos<R>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
+      tile[tile_pos<R, GPB>(line, r2)] = make_float2(pre[i].x, pre[i].y);
+      tile[tile_pos<R, GPB>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
     }
     if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
       const float2* nb = jbase + (size_t)(p + 1) * N * N;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        const int c = threadIdx.x + 256 * i;
+        const int c = threadIdx.x + NT * i;
         const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
         pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * N + y0 + r2);
       }
@@ -570,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv(const JobDesc* __restrict__ j
     lds_barrier();
     pk2 v[R];
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = to_pk(tile[tile_pos<R>(t + R * jj, grp)]);
+    for (int jj = 0; jj < R; ++jj) v[jj] = to_pk(tile[tile_pos<R, GPB>(t + R * jj, grp)]);
     lds_barrier();  // tile consumed: reuse it as transpose scratch
     fft_group<R, true>(v, t, PaddedScratch<R>{tile + grp * R * (R + 1)}, tw);
 #pragma unroll
@@ -709,9 +747,9 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
   {
-    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / GPB);
+    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R));
     if (tm) tm->begin(0, st);
-    hipLaunchKernelGGL(k_rowfwd<R>, dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
+    hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);
     if (tm) tm->end(0, n_jobs, st);
   }
@@ -741,15 +779,15 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if (tm) tm->end(1, n_jobs, st);
   }
   {
-    const unsigned blocks = (unsigned)n_jobs * (N / GPB);
+    const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
-    hipLaunchKernelGGL(k_rowinv<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
+    hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                        target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
                        field_out, target ? ~(size_t)0 : (size_t)0);
     if (tm) tm->end(2, n_jobs, st);
   }
   hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial,
-                     n_jobs, N / GPB, pd.job_stats);
+                     n_jobs, N / (kRowNT<R> / R), pd.job_stats);
   return hipGetLastError();
 }
 
