@@ -184,6 +184,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&p->delta, (size_t)max_jobs * sizeof(double)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "delta");
   if (hipMalloc(&pd.psf_partial, (size_t)max_jobs * hbx::kPsfBlocks * 2 * sizeof(double)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "psf partials");
+  if (hipMalloc(&pd.psf_order, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "psf order");
   if (hipMalloc(&pd.zero_row, (size_t)N * sizeof(float)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "zero row");
   if (hipMemcpy(pd.tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
@@ -210,6 +212,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->delta) (void)hipFree(p->delta);
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
+  if (p->pd.psf_order) (void)hipFree(p->pd.psf_order);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
                   (void*)p->map_d4, (void*)p->map_part, (void*)p->map_x, (void*)p->map_s, (void*)p->map_y})

@@ -46,6 +46,7 @@ struct PlanDev {
   double* job_stats;   // [max_jobs][3]
   float2* hpsf;        // [G][N][N] single-pixel field h_g = IFFT2(H_g) (lazy, incremental mode)
   double* psf_partial; // [max_jobs][kPsfBlocks][2]
+  int32_t* psf_order;  // [max_jobs] jobs sorted by colour group (launch order)
   float* zero_row;     // [N] zeros: the target row of a propagation without a target
   PassTimer* timer;    // nullable
 };
