@@ -663,6 +663,57 @@ int hbx_commit_flip(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, 
   return HBX_OK;
 }
 
+int hbx_eval_flips_psf(hbx_plan_t p, const uint64_t* base_mask, const float* target,
+                       const double* base_chan_stats, const float* field, const float* intensity,
+                       const int64_t* flips, int32_t K, double* psnr_out, double* group_stats,
+                       void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !target || !base_chan_stats || !field || !intensity || !flips || !psnr_out)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  rc = ensure_hpsf(p, st);
+  if (rc) return rc;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  for (int k0 = 0; k0 < K; k0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, K - k0);
+    HBX_HIP(hbx::launch_jobs_from_flips(flips + k0, n, N, N, P, CH, p->jobs, st));
+    HBX_HIP(hbx::launch_psf_eval(pd, p->jobs, n, base_mask, reinterpret_cast<const float2*>(field), intensity,
+                                 target, base_chan_stats, st));
+    HBX_HIP(hbx::launch_eval_finalize(p->jobs, pd.job_stats, n, G, base_chan_stats, psnr_out + k0,
+                                      group_stats ? group_stats + (size_t)k0 * 3 : nullptr,
+                                      pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
+  }
+  return HBX_OK;
+}
+
+int hbx_commit_flip_psf(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, double* prev_psnr,
+                        float* field, float* intensity, const int64_t* flips, const double* psnr_out,
+                        const double* group_stats, const int32_t* k, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !base_chan_stats || !prev_psnr || !field || !intensity || !flips || !psnr_out ||
+      !group_stats || !k)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  rc = ensure_hpsf(p, st);
+  if (rc) return rc;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  // toggle the mask bit first: the field update's delta is read from the new bit
+  HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
+                                  0x7fffffff, G, P, N, N, st));
+  HBX_HIP(hbx::launch_job_from_flip_k(flips, k, N, N, P, CH, p->jobs, pd.psf_order, p->accept_flag, st));
+  // psf_order is already {0}: launch_psf_commit visits the single job
+  HBX_HIP(hbx::launch_psf_commit(pd, p->jobs, 1, base_mask, reinterpret_cast<float2*>(field), intensity,
+                                 p->accept_flag, st));
+  return HBX_OK;
+}
+
 }  // extern "C"
 
 extern "C" {

@@ -104,6 +104,8 @@ hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W,
                                     JobDesc* jobs, int32_t* err, hipStream_t st);
 hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int P, int CH,
                                   JobDesc* jobs, hipStream_t st);
+hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int H, int W, int P, int CH,
+                                  JobDesc* jobs, int32_t* order, int32_t* accept, hipStream_t st);
 hipError_t launch_jobs_full(const int32_t* env_ids, int n_ids, int G, JobDesc* jobs, hipStream_t st);
 hipError_t launch_full_finalize(const JobDesc* jobs, const double* job_stats, int n_ids, int G,
                                 double* chan_stats, double* psnr, double count, int rel, double peak,

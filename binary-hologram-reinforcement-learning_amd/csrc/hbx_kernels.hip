@@ -63,6 +63,24 @@ __global__ void k_jobs_from_flips(const int64_t* __restrict__ flips, int K, int 
   jobs[k] = jd;
 }
 
+// the one job of candidate flips[*k] (commit of a speculative batch)
+__global__ void k_job_from_flip_k(const int64_t* __restrict__ flips, const int32_t* __restrict__ k,
+                                  int H, int W, int P, int CH, JobDesc* __restrict__ jobs,
+                                  int32_t* __restrict__ order, int32_t* __restrict__ accept) {
+  const int64_t a = flips[*k];
+  const int64_t hw = (int64_t)H * W;
+  JobDesc jd;
+  if (a < 0 || a >= (int64_t)CH * hw) {
+    jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
+  } else {
+    const int ch = (int)(a / hw);
+    jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(a % hw);
+  }
+  jobs[0] = jd;
+  order[0] = 0;
+  accept[0] = 1;
+}
+
 // full-propagation jobs: (env_ids[i], g) for all groups
 __global__ void k_jobs_full(const int32_t* __restrict__ env_ids, int n_ids, int G,
                             JobDesc* __restrict__ jobs) {
@@ -363,6 +381,11 @@ hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int
                                   JobDesc* jobs, hipStream_t st) {
   hipLaunchKernelGGL(k_jobs_from_flips, dim3((K + 127) / 128), dim3(128), 0, st, flips, K, H, W, P,
                      CH, jobs);
+  return hipGetLastError();
+}
+hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int H, int W, int P, int CH,
+                                  JobDesc* jobs, int32_t* order, int32_t* accept, hipStream_t st) {
+  hipLaunchKernelGGL(k_job_from_flip_k, dim3(1), dim3(1), 0, st, flips, k, H, W, P, CH, jobs, order, accept);
   return hipGetLastError();
 }
 hipError_t launch_jobs_full(const int32_t* env_ids, int n_ids, int G, JobDesc* jobs, hipStream_t st) {

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "hbx_plan_workspace_bytes", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
+    "hbx_eval_flips_psf", "hbx_commit_flip_psf",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -94,6 +95,8 @@ def _declare(lib):
     lib.hbx_field_refresh.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, VP]
     lib.hbx_simulate.argtypes = [VP, VP, I32, VP, VP, VP]
     lib.hbx_flip_map.argtypes = [VP, VP, VP, VP, VP, VP]
+    lib.hbx_eval_flips_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, I32, VP, VP, VP]
+    lib.hbx_commit_flip_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]

@@ -64,8 +64,15 @@ def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
 
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
-           stream=None) -> GreedyResult:
-    """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32."""
+           stream=None, mode: str = "fft", refresh_every: int = 4096) -> GreedyResult:
+    """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
+
+    mode="fft": every candidate is a full propagation of its colour group.
+    mode="psf": candidates are evaluated on the incremental-field path
+    (hbx_eval_flips_psf: one streaming pass over one plane); the base fields
+    are re-propagated exactly every ``refresh_every`` accepted flips."""
+    if mode not in ("fft", "psf"):
+        raise ValueError(f"mode must be 'fft' or 'psf', got {mode!r}")
     dev = plan.device
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
@@ -74,6 +81,11 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
                                      stream=stream)
     base_stats = stats[0].contiguous()
     prev_dev = psnr0.clone()
+    field = inten = None
+    if mode == "psf":
+        fc, it = plan.simulate(mask.unsqueeze(0), want_intensity=True, stream=stream)
+        field = torch.view_as_real(fc[0]).contiguous()
+        inten = it[0].contiguous()
     init = float(psnr0.item())
     prev = init
     psnr_buf = torch.empty(k_max, dtype=torch.float64, device=dev)
@@ -88,7 +100,11 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     while pos < total:
         k = min(ctl.k, total - pos)
         flips = order_t[pos:pos + k]
-        plan.eval_flips(mask, target, base_stats, flips, psnr_buf[:k], gst_buf[:k], stream=stream)
+        if mode == "psf":
+            plan.eval_flips_psf(mask, target, base_stats, field, inten, flips, psnr_buf[:k], gst_buf[:k],
+                                stream=stream)
+        else:
+            plan.eval_flips(mask, target, base_stats, flips, psnr_buf[:k], gst_buf[:k], stream=stream)
         launches += 1
         ps = psnr_buf[:k].cpu().numpy()
         i = first_improving(ps, prev)
@@ -99,8 +115,22 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
             continue
         last = float(ps[i])
         kdev.fill_(i)
-        plan.commit_flip(mask, base_stats, prev_dev, flips, psnr_buf, gst_buf, kdev, stream=stream)
+        if mode == "psf":
+            plan.commit_flip_psf(mask, base_stats, prev_dev, field, inten, flips, psnr_buf, gst_buf, kdev,
+                                 stream=stream)
+        else:
+            plan.commit_flip(mask, base_stats, prev_dev, flips, psnr_buf, gst_buf, kdev, stream=stream)
         prev = float(ps[i])
+        if mode == "psf" and refresh_every and (len(acc_pos) + 1) % refresh_every == 0:
+            # exact re-propagation bounds the fp32 drift of the incremental updates
+            _, stats, ps_exact = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                                stream=stream)
+            base_stats.copy_(stats[0])
+            prev_dev.copy_(ps_exact)
+            fc, it = plan.simulate(mask.unsqueeze(0), want_intensity=True, stream=stream)
+            field.copy_(torch.view_as_real(fc[0]))
+            inten.copy_(it[0])
+            prev = float(ps_exact.item())
         acc_pos.append(pos + i)
         acc_psnr.append(prev)
         acc_t.append(time.perf_counter() - t0)

@@ -237,6 +237,31 @@ class Plan:
                                            _stream(stream)), "hbx_eval_flips")
         return psnr_out, group_stats
 
+    def eval_flips_psf(self, base_mask, target, base_stats, field, intensity, flips,
+                       psnr_out=None, group_stats=None, stream=None):
+        """eval_flips on the incremental-field path: field [CH, H, W, 2] f32 and
+        intensity [G, H, W] f32 of the base state (from simulate)."""
+        c = self.cfg
+        _need(field, "field", torch.float32, (c.channels, c.height, c.width, 2), self.device)
+        _need(intensity, "intensity", torch.float32, (c.groups, c.height, c.width), self.device)
+        k = flips.shape[0]
+        _need(flips, "flips", torch.int64, (k,), self.device)
+        if psnr_out is None:
+            psnr_out = torch.empty((k,), dtype=torch.float64, device=self.device)
+        if group_stats is None:
+            group_stats = torch.empty((k, 3), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_eval_flips_psf(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                               _ptr(field), _ptr(intensity), _ptr(flips), k, _ptr(psnr_out),
+                                               _ptr(group_stats), _stream(stream)), "hbx_eval_flips_psf")
+        return psnr_out, group_stats
+
+    def commit_flip_psf(self, base_mask, base_stats, prev_psnr, field, intensity, flips, psnr_out,
+                        group_stats, k_dev: torch.Tensor, stream=None):
+        _lib.check(self.lib.hbx_commit_flip_psf(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),
+                                                _ptr(field), _ptr(intensity), _ptr(flips), _ptr(psnr_out),
+                                                _ptr(group_stats), _ptr(k_dev), _stream(stream)),
+                   "hbx_commit_flip_psf")
+
     def commit_flip(self, base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats,
                     k_dev: torch.Tensor, stream=None):
         _lib.check(self.lib.hbx_commit_flip(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),

@@ -206,6 +206,21 @@ int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stat
                     double* prev_psnr, const int64_t* flips, const double* psnr_out,
                     const double* group_stats, const int32_t* k, void* stream);
 
+/* hbx_eval_flips / hbx_commit_flip on the incremental-field path: the base
+ * env additionally carries its per-plane field [CH][H][W][2] and group
+ * intensities [G][H][W] (hbx_simulate), so a candidate costs one streaming
+ * pass over one plane (no FFT) -- the speculative greedy DBS of
+ * DBS_1024_24.py:313-422 at ~16 B/px per candidate.  The commit also rewrites
+ * the accepted plane's field and its group intensity. */
+int hbx_eval_flips_psf(hbx_plan_t plan, const uint64_t* base_mask, const float* target,
+                       const double* base_chan_stats, const float* field, const float* intensity,
+                       const int64_t* flips, int32_t K, double* psnr_out, double* group_stats,
+                       void* stream);
+int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stats,
+                        double* prev_psnr, float* field, float* intensity, const int64_t* flips,
+                        const double* psnr_out, const double* group_stats, const int32_t* k,
+                        void* stream);
+
 /* Incremental-field ("PSF") mode (reported separately from
  * the FFT-mode headline).  tt.simulate is linear, so flipping pixel (c, r, col)
  * changes only plane c's field, by delta * h_g shifted to (r, col), where

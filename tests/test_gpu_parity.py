@@ -518,3 +518,22 @@ def test_premodel_on_gpu_feeds_env_reset():
     base = env.reset(pre, tgt[0].numpy())
     assert abs(float(vec.state.init_psnr[0].item()) - base) <= PSNR_TOL
     vec.close()
+
+
+@pytest.mark.parametrize("refresh", [0, 64])
+def test_dbs_greedy_incremental_mode(golden_dir, refresh):
+    """Greedy DBS with candidates on the incremental-field path
+    (hbx_eval_flips_psf / hbx_commit_flip_psf): the serial accept sequence of
+    the 4096-flip oracle trace, with and without periodic exact refresh."""
+    import hbx
+    from hbx import dbs
+    d = load(golden_dir, "dbs_trace_64.npz")
+    plan = hbx.Plan(dev_cfg(small_rgb()), max_jobs=128)
+    mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
+    res = dbs.greedy(plan, mask, torch.from_numpy(d["target"]).cuda(), d["order"], mode="psf",
+                     refresh_every=refresh)
+    want_pos = np.nonzero(d["accepted"])[0]
+    got = np.array(res.accepted_positions)
+    assert len(got) == len(want_pos) and np.array_equal(got, want_pos)
+    assert abs(res.final_psnr - float(d["final_psnr"])) <= PSNR_TOL
+    assert np.array_equal(mask.cpu().numpy().view("<u8"), d["final_mask_bits"])
