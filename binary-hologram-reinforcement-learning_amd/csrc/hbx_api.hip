@@ -105,7 +105,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (o->height == 1024) R = 32;
   else if (o->height == 256) R = 16;
   else if (o->height == 64) R = 8;
-  else return fail(HBX_ERR_UNSUPPORTED, "N must be 64, 256 or 1024");
+  else if (o->height == 896) R = 0;   // crop of a 1024 mask: generic 28 x 32 path
+  else return fail(HBX_ERR_UNSUPPORTED, "N must be 64, 256, 896 or 1024");
   if (o->groups < 1 || o->groups > HBX_MAX_GROUPS) return fail(HBX_ERR_INVALID, "groups out of range");
   if (o->planes < 2 || (o->planes % 2)) return fail(HBX_ERR_INVALID, "planes must be even and >= 2");
   if (max_jobs < o->groups) return fail(HBX_ERR_INVALID, "max_jobs must be >= groups");
@@ -137,6 +138,12 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       const double a = -2.0 * M_PI * (double)((t * k1) % N) / (double)N;
       tw[(size_t)k1 * R + t] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
+  if (R == 0)   // N = 896: [k1 < 28][t < 32] = W896^{t k1}
+    for (int k1 = 0; k1 < 28; ++k1)
+      for (int t = 0; t < 32; ++t) {
+        const double a = -2.0 * M_PI * (double)(t * k1) / (double)N;
+        tw[(size_t)k1 * 32 + t] = make_float2((float)std::cos(a), (float)std::sin(a));
+      }
   if (N == 1024) {  // whole-wave FFT tables of the column pass: tw1[k1][L], tw2[m1][l0]
     for (int k1 = 0; k1 < 16; ++k1)
       for (int L = 0; L < 64; ++L) {
@@ -161,8 +168,10 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
         ht[g * hrow + (size_t)kx * N + ky] = make_float2((float)h.real(), (float)h.imag());
       }
     }
-  const int RB = N / (256 / R);
-  const size_t ws_a_bytes = (size_t)max_jobs * P * (N / 2) * N * sizeof(float2);
+  // partial slots per job: row blocks of the last pass (8 rows each on the generic path)
+  const int RB = R ? N / (256 / R) : N / 8;
+  // the generic path ping-pongs full planes between A and B
+  const size_t ws_a_bytes = (size_t)max_jobs * P * (R ? N / 2 : N) * N * sizeof(float2);
   const size_t ws_b_bytes = (size_t)max_jobs * P * N * N * sizeof(float2);
   p->ws_bytes = ws_a_bytes + ws_b_bytes;
   auto cleanup = [&](int code, const std::string& msg) {

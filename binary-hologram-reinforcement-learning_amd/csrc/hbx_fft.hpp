@@ -462,4 +462,136 @@ __device__ __forceinline__ void wave_fft1024_inv(float2 (&v)[16], int L, float2*
   dft_reg<16, true>(v);
 }
 
+// ---------------------------------------------------------------------------
+// N = 896 (the 64-pixel crop of a 1024 mask, env_1024_24_128.py:144-149):
+// 896 = 28 x 32, so a 32-lane group does a four-step with 28 registers in the
+// first stage and 32 in the second:
+//   natural layout: lane t < 32, register j < 28 holds x[t + 32 j]
+//   slot layout:    lane k1 < 28, register k2 < 32 holds X[k1 + 28 k2]
+// The 28-point DFT is Good-Thomas (28 = 4 x 7, coprime: no twiddles, only
+// index maps n = (7 n1 + 4 n2) mod 28, k = (21 k1 + 8 k2) mod 28); the
+// 7-point DFT pairs x_m with x_{7-m}.  Lanes 28..31 carry no data in the slot
+// layout (their registers are don't-care).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float c7(int k) {
+  switch (((k % 7) + 7) % 7) {
+    case 0: return 1.0f;
+    case 1: case 6: return 0.62348980185873353053f;
+    case 2: case 5: return -0.22252093395631440429f;
+    default: return -0.90096886790241912624f;
+  }
+}
+__device__ __forceinline__ float s7(int k) {   // sin(2 pi k / 7)
+  switch (((k % 7) + 7) % 7) {
+    case 0: return 0.0f;
+    case 1: return 0.78183148246802980871f;
+    case 2: return 0.97492791218182360702f;
+    case 3: return 0.43388373911755812048f;
+    case 4: return -0.43388373911755812048f;
+    case 5: return -0.97492791218182360702f;
+    default: return -0.78183148246802980871f;
+  }
+}
+
+// in-place 7-point DFT of x[0..6] (forward: exp(-2 pi i n k / 7))
+template <bool INV>
+__device__ __forceinline__ void dft7(float2 (&x)[7]) {
+  float2 a[4], b[4];
+#pragma unroll
+  for (int m = 1; m <= 3; ++m) { a[m] = cadd(x[m], x[7 - m]); b[m] = csub(x[m], x[7 - m]); }
+  const float2 x0 = x[0];
+  x[0] = cadd(x0, cadd(a[1], cadd(a[2], a[3])));
+#pragma unroll
+  for (int k = 1; k <= 3; ++k) {
+    float2 u = x0, w = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int m = 1; m <= 3; ++m) {
+      const float c = c7(m * k), sn = s7(m * k);
+      u = make_float2(fmaf(c, a[m].x, u.x), fmaf(c, a[m].y, u.y));
+      w = make_float2(fmaf(sn, b[m].x, w.x), fmaf(sn, b[m].y, w.y));
+    }
+    // forward: X[k] = u - i w, X[7-k] = u + i w ; inverse swaps them
+    const float2 miw = make_float2(w.y, -w.x);
+    x[k] = INV ? csub(u, miw) : cadd(u, miw);
+    x[7 - k] = INV ? cadd(u, miw) : csub(u, miw);
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2& x0, float2& x1, float2& x2, float2& x3) {
+  const float2 t0 = cadd(x0, x2), t1 = csub(x0, x2), t2 = cadd(x1, x3), t3 = csub(x1, x3);
+  // forward: X1 = t1 - i t3, X3 = t1 + i t3
+  const float2 mi3 = INV ? make_float2(-t3.y, t3.x) : make_float2(t3.y, -t3.x);
+  x0 = cadd(t0, t2);
+  x2 = csub(t0, t2);
+  x1 = cadd(t1, mi3);
+  x3 = csub(t1, mi3);
+}
+
+// 28-point DFT of v[0..27], natural order in and out (Good-Thomas 4 x 7)
+template <bool INV>
+__device__ __forceinline__ void dft28(float2 (&v)[32]) {
+  float2 y[4][7];
+#pragma unroll
+  for (int n2 = 0; n2 < 7; ++n2) {
+    float2 e0 = v[(4 * n2) % 28], e1 = v[(7 + 4 * n2) % 28];
+    float2 e2 = v[(14 + 4 * n2) % 28], e3 = v[(21 + 4 * n2) % 28];
+    dft4<INV>(e0, e1, e2, e3);
+    y[0][n2] = e0; y[1][n2] = e1; y[2][n2] = e2; y[3][n2] = e3;
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    dft7<INV>(y[k1]);
+#pragma unroll
+    for (int k2 = 0; k2 < 7; ++k2) v[(21 * k1 + 8 * k2) % 28] = y[k1][k2];
+  }
+}
+
+// 896-point FFT by 32 lanes, natural layout in -> slot layout out.
+// tw896: LDS [k1 < 28][t < 32] = W896^{t k1} (forward sign); INV conjugates.
+template <bool INV, class Scratch>
+__device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+  asm volatile("" ::: "memory");
+  dft28<INV>(v);
+#pragma unroll
+  for (int k1 = 1; k1 < 28; ++k1) {
+    const float2 w = tw896[k1 * 32 + t];
+    v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+  }
+  wave_sync();
+#pragma unroll
+  for (int k1 = 0; k1 < 28; ++k1) *sc.at(t, k1) = v[k1];
+  wave_sync();
+  // lane k1 (< 28) gathers A'[t][k1] for t = 0..31; lanes 28..31 read in-range junk
+  const int k1 = t < 28 ? t : 0;
+#pragma unroll
+  for (int tt = 0; tt < 32; ++tt) v[tt] = *sc.at(tt, k1);
+  wave_sync();
+  dft_reg<32, INV>(v);
+}
+
+// 896-point FFT by 32 lanes, slot layout in -> natural layout out (adjoint of
+// fft896_ns: the same stages in reverse order with the opposite sign)
+template <bool INV, class Scratch>
+__device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+  asm volatile("" ::: "memory");
+  dft_reg<32, INV>(v);        // over k2 -> index t (the natural lane)
+  wave_sync();
+  // lane k1 (< 28) holds B[k1][t] for t = 0..31 in v[t]
+  if (t < 28) {
+#pragma unroll
+    for (int tt = 0; tt < 32; ++tt) *sc.at(tt, t) = v[tt];
+  }
+  wave_sync();
+#pragma unroll
+  for (int k1 = 0; k1 < 28; ++k1) v[k1] = *sc.at(t, k1);
+  wave_sync();
+#pragma unroll
+  for (int k1 = 1; k1 < 28; ++k1) {
+    const float2 w = tw896[k1 * 32 + t];
+    v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+  }
+  dft28<INV>(v);              // over k1 -> register j: x[t + 32 j]
+}
+
 }  // namespace hbx

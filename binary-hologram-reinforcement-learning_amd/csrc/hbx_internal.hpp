@@ -34,7 +34,7 @@ struct PassTimer {
 };
 
 struct PlanDev {
-  int R;               // N = R * R
+  int R;               // N = R * R; 0: N = 896 = 28 x 32 (generic path)
   int N, G, P;
   float va, vb;        // field = va + vb * bit
   float2* tw;          // [N]  W_N^{t k1} at [k1 * R + t]; N = 1024 appends the
@@ -83,6 +83,10 @@ struct EnvParams {
 // field_out (nullable): [env][G*P][N][N] complex field of every propagated plane
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, float2* field_out, hipStream_t st);
+// generic propagation (N = 896, hbx_generic.hip): prep -> 2-D FFT -> H -> inverse
+// 2-D FFT -> |U|^2 mean + partial sums, on the transposing row-FFT kernel
+hipError_t run_jobs_generic(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
+                            const float* target, float* inten_out, float2* field_out, hipStream_t st);
 // 2-D FFT of n_planes [N][N] complex planes in a (result in a; b is scratch of
 // the same size).  Unnormalised both ways.
 hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,

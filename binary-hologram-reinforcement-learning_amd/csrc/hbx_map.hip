@@ -41,7 +41,7 @@ __device__ __forceinline__ double psnr_of(double sxy, double sxx, double syy, do
 
 __device__ __forceinline__ size_t neg_index(size_t i, int N) {  // (-ky, -kx) mod N
   const int ky = (int)(i / N), kx = (int)(i % N);
-  return (size_t)((N - ky) & (N - 1)) * N + ((N - kx) & (N - 1));
+  return (size_t)((N - ky) % N) * N + ((N - kx) % N);
 }
 
 // h-side functions of every group: [g][4][N][N] = h, |h|^2, |h|^2 h, h^2

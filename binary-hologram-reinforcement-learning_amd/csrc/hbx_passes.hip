@@ -720,9 +720,64 @@ static hipError_t launch_fft2d(const PlanDev& pd, float2* a, float2* b, int n_pl
   return hipGetLastError();
 }
 
+// N = 896 (crop of a 1024 mask): the same transposing row pass on the 28 x 32
+// lane-group FFT (natural layout in, slot layout out: lane k1 < 28 writes
+// X[k1 + 28 k2] into the tile)
+template <bool INV>
+__global__ __launch_bounds__(256, 2) void k_fft_rt896(const float2* __restrict__ in,
+                                                      float2* __restrict__ out,
+                                                      const float2* __restrict__ tw_glob) {
+  constexpr int N = 896, R = 32, GPB = 8, RB = N / GPB;
+  constexpr int SCR = GPB * R * (R + 1);
+  static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
+  __shared__ float2 tw[N];
+  __shared__ __attribute__((aligned(16))) float2 lds[SCR];
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  int bid = xcd_pair<RB>(blockIdx.x);
+  const int rb = bid % RB;
+  const int plane = bid / RB;
+  const int y0 = rb * GPB;
+  const float2* row = in + ((size_t)plane * N + y0 + grp) * N + t;
+  float2 v[32];
+#pragma unroll
+  for (int j = 0; j < 28; ++j) v[j] = row[R * j];
+  __syncthreads();  // tw visible
+  fft896_ns<INV>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
+  lds_barrier();
+  if (t < 28) {
+#pragma unroll
+    for (int k2 = 0; k2 < 32; ++k2) lds[tile_pos<R, GPB>(t + 28 * k2, grp)] = v[k2];
+  }
+  lds_barrier();
+  float2* base = out + (size_t)plane * N * N;
+  constexpr int CHUNKS = N * GPB / 2;
+  static_assert(CHUNKS % 256 == 0, "chunking");
+#pragma unroll
+  for (int i = 0; i < CHUNKS / 256; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int r2 = (c % (GPB / 2)) * 2;
+    const int line = c / (GPB / 2);
+    const float2 a = lds[tile_pos<R, GPB>(line, r2)];
+    const float2 b = lds[tile_pos<R, GPB>(line, r2 + 1)];
+    *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
 hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,
                      hipStream_t st) {
   if (n_planes <= 0) return hipSuccess;
+  if (pd.R == 0) {   // N = 896
+    const unsigned blocks = (unsigned)n_planes * (896 / 8);
+    for (int pass = 0; pass < 2; ++pass) {
+      const float2* src = pass == 0 ? a : b;
+      float2* dst = pass == 0 ? b : a;
+      if (inverse) hipLaunchKernelGGL((k_fft_rt896<true>), dim3(blocks), dim3(256), 0, st, src, dst, pd.tw);
+      else hipLaunchKernelGGL((k_fft_rt896<false>), dim3(blocks), dim3(256), 0, st, src, dst, pd.tw);
+    }
+    return hipGetLastError();
+  }
   switch (pd.R) {
     case 32: return launch_fft2d<32>(pd, a, b, n_planes, inverse, st);
     case 16: return launch_fft2d<16>(pd, a, b, n_planes, inverse, st);
@@ -793,6 +848,9 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
 
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, float2* field_out, hipStream_t st) {
+  if (pd.R == 0)
+    return run_jobs_generic(pd, jobs, n_jobs, reinterpret_cast<const uint64_t*>(mask), target, inten_out,
+                            field_out, st);
   switch (pd.R) {
     case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
     case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);

@@ -34,7 +34,7 @@ __device__ __forceinline__ float flip_delta(const uint64_t* mask, const JobDesc&
 
 // |d| mod N folded into [0, N/2] (h is even in each coordinate)
 __device__ __forceinline__ int fold(int d, int N) {
-  d &= N - 1;
+  d = (N & (N - 1)) ? ((d % N) + N) % N : (d & (N - 1));   // N = 896 is not a power of 2
   return d <= N / 2 ? d : N - d;
 }
 

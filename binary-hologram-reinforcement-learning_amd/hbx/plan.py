@@ -108,6 +108,29 @@ def unpack_bits(words: torch.Tensor, width: int) -> torch.Tensor:
     return bits.reshape(*words.shape[:-1], width).to(torch.int8)
 
 
+def crop(t: torch.Tensor, margin: int = 64) -> torch.Tensor:
+    """Centre crop of ``margin`` pixels per side on the last two axes
+    (env_1024_24_128.py:144-149, DBS_1024_24-128.py:210-216); 1024 -> 896."""
+    if margin <= 0:
+        return t
+    return t[..., margin:-margin, margin:-margin].contiguous()
+
+
+def crop_bits(words: torch.Tensor, margin: int = 64) -> torch.Tensor:
+    """The same crop on packed masks [..., H, W/64]: a 64-aligned margin drops
+    whole words, so this is a strided copy (no unpacking)."""
+    if margin % 64:
+        raise ValueError("crop_bits needs a margin that is a multiple of 64")
+    k = margin // 64
+    return words[..., margin:-margin, k:-k].contiguous()
+
+
+def crop_config(cfg: "OpticsConfig", margin: int = 64) -> "OpticsConfig":
+    """Optics of the cropped mask: same physics, N - 2 * margin pixels."""
+    import dataclasses
+    return dataclasses.replace(cfg, height=cfg.height - 2 * margin, width=cfg.width - 2 * margin)
+
+
 class Plan:
     """hbx_plan_t owner.  ``max_jobs`` bounds the group propagations in flight
     (workspace = max_jobs * planes * N^2 * 8 bytes)."""

@@ -537,3 +537,112 @@ def test_dbs_greedy_incremental_mode(golden_dir, refresh):
     assert len(got) == len(want_pos) and np.array_equal(got, want_pos)
     assert abs(res.final_psnr - float(d["final_psnr"])) <= PSNR_TOL
     assert np.array_equal(mask.cpu().numpy().view("<u8"), d["final_mask_bits"])
+
+
+# ---------------------------------------------------------------------------
+# N = 896: the 64-pixel crop of a 1024 mask (env_1024_24_128.py:144-149,
+# DBS_1024_24-128.py:210-216) on the generic 28 x 32 mixed-radix path
+# ---------------------------------------------------------------------------
+def _crop_inputs(seed):
+    import hbx
+    full = O.rgb_config(1024)
+    pre, tgt = O.synthetic_inputs(full, seed)
+    ocfg = O.rgb_config(896)
+    pre_c, tgt_c = O.crop(pre, 64), O.crop(tgt, 64)
+    bits_full = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    bits = hbx.crop_bits(bits_full, 64)
+    return ocfg, pre_c, tgt_c, bits
+
+
+def test_crop_896_propagate_vs_oracle():
+    import hbx
+    ocfg, pre, tgt, bits = _crop_inputs(7)
+    mask = (pre >= 0.5).astype(np.uint8)
+    assert np.array_equal(bits.cpu().numpy().view("<u8"), O.pack_mask(mask))
+    prop = O.Propagator(ocfg)
+    ref_i = prop.all_intensity(mask)
+    ref_st = np.stack([O.chan_stats(ref_i[g], tgt[g]) for g in range(3)])
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=6)
+    inten, stats, psnr = plan.propagate(bits[None], torch.from_numpy(tgt).cuda()[None])
+    torch.cuda.synchronize()
+    assert np.allclose(stats[0].cpu().numpy(), ref_st, rtol=STATS_RTOL)
+    assert abs(float(psnr[0]) - prop.psnr(ref_st)) <= PSNR_TOL
+    got = inten[0].cpu().numpy()
+    assert np.max(np.abs(got - ref_i)) <= 2e-5 * np.max(ref_i)
+    plan.close()
+
+
+@pytest.mark.parametrize("field_kind", [O.FIELD_AMPLITUDE, O.FIELD_PHASE])
+def test_crop_896_eval_flips_and_map_vs_oracle(field_kind):
+    import hbx
+    _, pre, tgt, bits = _crop_inputs(8)
+    ocfg = O.rgb_config(896, field_kind=field_kind)
+    env = O.OracleEnv(ocfg)
+    base = env.reset(pre, tgt)
+    n = 896 * 896
+    flips = np.array([0, n - 1, 895, n - 896, 5 * n + 448 * 896 + 447, 13 * n + 77, 24 * n - 1], np.int64)
+    want = np.array([env.evaluate_flip(int(a))[0] for a in flips])
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=8)
+    t = torch.from_numpy(tgt).cuda()
+    _, st, p0 = plan.propagate(bits[None], t[None])
+    assert abs(float(p0[0]) - base) <= PSNR_TOL
+    got, _ = plan.eval_flips(bits, t, st[0].contiguous(), torch.from_numpy(flips).cuda())
+    assert np.max(np.abs(got.cpu().numpy() - want)) <= PSNR_TOL
+    dmap, b = plan.flip_map(bits, t)
+    assert abs(float(b.item()) - base) <= PSNR_TOL
+    assert bool(torch.isfinite(dmap).all())
+    d = dmap.reshape(-1)[torch.from_numpy(flips).cuda()].double().cpu().numpy()
+    assert np.max(np.abs(d - (want - base))) <= MAP_TOL
+    plan.close()
+
+
+def test_crop_896_psf_matches_fft():
+    """Incremental-field mode at 896 (folded h offsets, non-power-of-2 N)
+    agrees with the FFT mode step by step."""
+    import hbx
+    from hbx.env import HologramVecEnv
+    cfg = hbx.rgb_config(896)
+    B = 2
+    gens = [torch.Generator(device="cuda").manual_seed(70 + i) for i in range(B)]
+    pres = [torch.rand((24, 896, 896), generator=g, device="cuda") for g in gens]
+    tgts = [torch.rand((3, 896, 896), generator=g, device="cuda") for g in gens]
+    kw = dict(pre_model_source=lambda i: pres[i], obs_keys=(), auto_reset=False)
+    fft = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    psf = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="psf", refresh_every=8, **kw)
+    fft.reset()
+    psf.reset()
+    assert torch.allclose(fft.state.init_psnr, psf.state.init_psnr, atol=1e-9)
+    acts = torch.randint(0, 24 * 896 * 896, (24, B), generator=gens[0], device="cuda")
+    for k in range(24):
+        _, p1, a1, _, _ = fft.step_device(acts[k])
+        _, p2, a2, _, _ = psf.step_device(acts[k])
+        assert torch.max(torch.abs(p1 - p2)).item() <= PSNR_TOL
+    assert torch.equal(fft.state.mask, psf.state.mask)
+    fft.close()
+    psf.close()
+
+
+def test_crop_896_dbs_greedy_vs_oracle():
+    """DBS on the crop (DBS_1024_24-128.py:210-300): FFT-mode and
+    incremental-mode greedy runs against the serial f64 oracle."""
+    import hbx
+    from hbx import dbs
+    ocfg, pre, tgt, bits = _crop_inputs(9)
+    env = O.OracleEnv(ocfg)
+    env.reset(pre, tgt)
+    order = np.random.default_rng(3).integers(0, 24 * 896 * 896, 40)
+    acc, psnrs, final = O.dbs_greedy(env, order)
+    prev = np.maximum.accumulate(np.concatenate([[env.initial_psnr], psnrs]))[:-1]
+    clear = np.abs(psnrs - prev) > 1e-5      # fp32 fields cannot order ties below this
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=16)
+    t = torch.from_numpy(tgt).cuda()
+    for mode in ("fft", "psf"):
+        m = bits.clone()
+        res = dbs.greedy(plan, m, t, order, mode=mode)
+        got = np.zeros(len(order), bool)
+        got[res.accepted_positions] = True
+        assert np.array_equal(got[clear], acc[clear]), mode
+        assert abs(res.final_psnr - final) <= PSNR_TOL, mode
+        if np.array_equal(got, acc):
+            assert np.array_equal(m.cpu().numpy().view("<u8"), O.pack_mask(env.state)), mode
+    plan.close()

@@ -183,3 +183,20 @@ def test_target_folder(tmp_path):
     assert t2.shape == (1, 3, 36, 36)
     tr = TargetFolder(str(tmp_path), ips=32, train=True, seed=3)
     assert tr[1][0].shape == (1, 3, 32, 32)
+
+
+def test_crop_bits_matches_oracle_crop():
+    """Packed 64-pixel crop (env_1024_24_128.py:144-149) == crop then pack."""
+    from hbx.plan import crop, crop_bits, pack_bits
+    m = (np.random.default_rng(4).random((2, 256, 256)) > 0.5).astype(np.uint8)
+    got = crop_bits(pack_bits(torch.from_numpy(m)), 64).numpy().view("<u8")
+    assert np.array_equal(got, O.pack_mask(O.crop(m, 64)))
+    assert np.array_equal(crop(torch.from_numpy(m), 64).numpy(), O.crop(m, 64))
+    with pytest.raises(ValueError):
+        crop_bits(pack_bits(torch.from_numpy(m)), 32)
+
+
+def test_crop_config():
+    import hbx
+    c = hbx.crop_config(hbx.rgb_config(1024), 64)
+    assert (c.height, c.width, c.groups, c.planes) == (896, 896, 3, 8)
