@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--psf-steps", type=int, default=200)
     ap.add_argument("--chunk", type=int, default=0,
                     help="jobs per launch sequence (0 = all envs at once)")
-    ap.add_argument("--dbs-flips", type=int, default=8192,
+    ap.add_argument("--dbs-flips", type=int, default=65536,
                     help="greedy-DBS prefix (flips of the shuffled order) timed on env 0's image, "
                          "SURVEY 8d cfg 2 (0 = skip)")
     ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")

@@ -28,6 +28,25 @@
 
 namespace hbx {
 
+// Precision study (SURVEY 8d cfg 5): `make exp EXP=BF16_STORE` / `EXP=F16_STORE` round every
+// value written to the two pass intermediates (row spectrum, column-pass output) to bf16 /
+// fp16, i.e. the numerics of half-width intermediate storage (the layout stays f32).  Never
+// part of the product build.
+__device__ __forceinline__ float2 store_round(float2 v) {
+#if defined(HBX_BF16_STORE)
+  auto r = [](float x) {
+    uint32_t u = __float_as_uint(x);
+    u += 0x7fffu + ((u >> 16) & 1u);   // round to nearest even
+    return __uint_as_float(u & 0xffff0000u);
+  };
+  return make_float2(r(v.x), r(v.y));
+#elif defined(HBX_F16_STORE)
+  return make_float2((float)(_Float16)v.x, (float)(_Float16)v.y);
+#else
+  return v;
+#endif
+}
+
 // Position of element (line, r) in an LDS tile [line][GPB rows], r XOR-swizzled
 // by a function of (line mod R) only: lane t of a group reading line t + R*j
 // then addresses base_t + j*R*GPB (immediate offsets, no per-j address VGPRs),
@@ -174,8 +193,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
     const int c = threadIdx.x + NT * i;
     const int r2 = (c % (GPB / 2)) * 2;
     const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
-    const float2 a = tile[tile_pos<R, GPB>(line, r2)];
-    const float2 b = tile[tile_pos<R, GPB>(line, r2 + 1)];
+    const float2 a = store_round(tile[tile_pos<R, GPB>(line, r2)]);
+    const float2 b = store_round(tile[tile_pos<R, GPB>(line, r2 + 1)]);
     *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
   }
 }
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     {
       float2* out = bout + (size_t)kx * N;
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = COL2_ST(v[k2]);
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = store_round(COL2_ST(v[k2]));
     }
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
       const float2* in = ain + (size_t)(kx + GPB) * N;
@@ -431,7 +450,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     {
       float2* out = bout + (size_t)(dc ? N / 2 : N - kx) * N;
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = COL2_ST(m[k2]);
+      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = store_round(COL2_ST(m[k2]));
     }
   }
 }
