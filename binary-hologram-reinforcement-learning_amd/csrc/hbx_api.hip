@@ -171,8 +171,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   // partial slots per job: row blocks of the last pass (8 rows each on the generic path)
   const int RB = R ? N / (256 / R) : N / 8;
   // the generic path ping-pongs full planes between A and B
-  const size_t ws_a_bytes = (size_t)max_jobs * P * (R ? N / 2 : N) * N * sizeof(float2);
-  const size_t ws_b_bytes = (size_t)max_jobs * P * N * N * sizeof(float2);
+  const size_t ws_a_bytes = (size_t)max_jobs * P * (R ? hbx::plane_a_elems(R) : (size_t)N * N) * sizeof(float2);
+  const size_t ws_b_bytes = (size_t)max_jobs * P * (R ? hbx::plane_b_elems(R) : (size_t)N * N) * sizeof(float2);
   p->ws_bytes = ws_a_bytes + ws_b_bytes;
   auto cleanup = [&](int code, const std::string& msg) {
     hbx_plan_destroy(p);

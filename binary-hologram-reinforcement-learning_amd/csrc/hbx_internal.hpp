@@ -14,6 +14,42 @@ struct JobDesc {
   int32_t flip_pix;    // row * W + col
 };
 
+// Intermediate layout of the fused N = R^2 path (hbx_passes.hip).  The row
+// passes run blocks of row_nt(R) threads = panel_rows(R) rows; a plane of L
+// lines is stored as N / PAN panels [L][PAN] (PAN = panel_rows), panel q at
+// q * panel_stride.  The pad keeps consecutive panels off the same memory
+// channel: a column-pass line touches one 64-B piece of every panel, and with
+// power-of-two panel strides those pieces all land on one channel.
+#ifndef HBX_ROW_NT
+#define HBX_ROW_NT 256
+#endif
+#ifndef HBX_PANEL_PAD
+#define HBX_PANEL_PAD 0
+#endif
+#ifndef HBX_PANEL_A   // rows per panel of A (0: one panel of N rows = column-major lines)
+#define HBX_PANEL_A 0
+#endif
+#ifndef HBX_PANEL_B   // rows per panel of B
+#define HBX_PANEL_B 16
+#endif
+__host__ __device__ constexpr int row_nt(int R) { return R == 32 ? HBX_ROW_NT : 256; }
+__host__ __device__ constexpr int panel_rows(int R) { return row_nt(R) / R; }
+__host__ __device__ constexpr int pan_of(int R, int rows) {
+  return rows <= 0 || rows >= R * R ? R * R : (rows < panel_rows(R) ? panel_rows(R) : rows);
+}
+__host__ __device__ constexpr int pan_a(int R) { return pan_of(R, HBX_PANEL_A); }
+__host__ __device__ constexpr int pan_b(int R) { return pan_of(R, HBX_PANEL_B); }
+__host__ __device__ constexpr int panel_stride(int R, int L, int PAN) {
+  return L * PAN + (PAN < R * R ? HBX_PANEL_PAD : 0);
+}
+// float2 elements per intermediate plane: A (half spectrum, N/2 lines), B (N lines)
+__host__ __device__ constexpr size_t plane_a_elems(int R) {
+  return (size_t)(R * R / pan_a(R)) * panel_stride(R, R * R / 2, pan_a(R));
+}
+__host__ __device__ constexpr size_t plane_b_elems(int R) {
+  return (size_t)(R * R / pan_b(R)) * panel_stride(R, R * R, pan_b(R));
+}
+
 // Optional hipEvent pairs around every pass launch (hbx_plan_set_timing).
 constexpr int kNumPasses = 5;  // rowfwd, col, rowinv, psf_eval, psf_commit
 struct PassTimer {

@@ -2,22 +2,25 @@
 //
 // One "job" = one colour group (P planes, N x N) of one env, propagated with
 // an optional single-pixel flip applied on the fly (env.py:164-172).  The
-// intermediates are COLUMN-MAJOR (a "line" kx holds the N values over y), so
-// the heavy column pass streams whole contiguous 8 KB lines and the two
-// transposes a 2-D FFT needs live in LDS tiles of the row passes:
+// intermediates are organised by spectral LINE kx (the N values over y), so
+// the column pass streams whole lines and the two transposes a 2-D FFT needs
+// live in LDS tiles of the row passes.  A is stored column-major ([kx][y]);
+// B in panels of 16 rows ([y / 16][kx][y % 16], hbx_internal.hpp), which gives
+// the column pass 256-B pieces to write and the row inverse pass 128-B pieces
+// to read (measured: 1-2 % over column-major B; 8-row panels made the column
+// pass's scattered 64-B writes cost 1 ms).
 //
 //   k_rowfwd  GPB rows of a plane pair per block: bits -> one complex FFT per
 //             row pair (plane a real, plane b imaginary) -> Hermitian split ->
 //             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0) ->
 //             LDS tile transpose -> A[kx][y0..y0+GPB)       [HBM: read N^2/8 B, write 4 N^2 B per plane]
-//   k_col     per half-spectrum line kx, two lane groups: FFT over y ->
-//             x H(kx, ky) -> IFFT -> B line kx, and (Hermitian symmetry)
-//             conj F(kx, -ky) H(kx, ky) -> IFFT -> B line N - kx (N/2 for
-//             kx = 0).  Lane groups loop over lines with the next input line
-//             prefetched into registers (no block barriers: A and B are
-//             separate buffers)                                  [read 4 N^2, write 8 N^2]
-//   k_rowinv  GPB rows per block, all P planes: LDS tile transpose of
-//             B[kx][y0..y0+GPB) (next plane's tile prefetched into registers
+//   k_col2    one lane group per half-spectrum line kx: FFT over y -> x H and
+//             x conj H (H is even in fx and ky) -> two IFFTs -> B lines kx
+//             and N - kx (N/2 for kx = 0); buffer loads / stores with one
+//             address VGPR per line; the next input line is prefetched under
+//             the second IFFT                                    [read 4 N^2, write 8 N^2]
+//   k_rowinv  GPB rows per block, all P planes: LDS tile transpose of the B
+//             rows y0..y0+GPB (next plane's tile prefetched into registers
 //             behind LDS-only barriers) -> IFFT over kx -> |U|^2 -> plane
 //             mean -> f64 partials of (I*T, I^2, T^2) vs the target row   [read 8 N^2 per plane + 4 N^2]
 #include <hip/hip_runtime.h>
@@ -66,15 +69,66 @@ __device__ __forceinline__ int tile_pos(int line, int r) {
   }
 }
 
-// Threads per block of the row passes at N = 1024.  -DHBX_ROW_NT=512 gives 16
-// rows per block (128-B pieces of every intermediate line, conflict-free
-// swizzle above) but only one 143-KB block per CU, whose barriers then stall
-// the whole CU: measured k_rowfwd 1.17 -> 1.54 ms, k_rowinv 2.01 -> 2.62 ms.
-#ifndef HBX_ROW_NT
-#define HBX_ROW_NT 256
-#endif
+// Threads per block of the row passes at N = 1024 (row_nt, hbx_internal.hpp).
+// -DHBX_ROW_NT=512 gives 16 rows per block (conflict-free swizzle above) but
+// only one 143-KB block per CU, whose barriers then stall the whole CU:
+// measured k_rowfwd 1.17 -> 1.54 ms, k_rowinv 2.01 -> 2.62 ms.
 template <int R>
-constexpr int kRowNT = (R == 32) ? HBX_ROW_NT : 256;
+constexpr int kRowNT = row_nt(R);
+
+// Intermediate layout (hbx_internal.hpp): panels of PAN = kRowNT / R rows, the
+// row passes' block height.  A plane of L lines (L = N/2 for A, N for B) is
+// N / PAN panels [L][PAN], element (line, y) at (y / PAN) * PS + line * PAN +
+// y % PAN with PS = panel_stride(R, L).  A row block then writes (k_rowfwd)
+// or reads (k_rowinv) ONE contiguous L * PAN * 8-B panel, while a column-pass
+// lane group sees line kx as 64-B pieces of PAN consecutive y -- two adjacent
+// lines per wave, so whole 128-B lines per wave instruction.
+template <int R>
+constexpr int kPanel = panel_rows(R);
+
+// Line kx of a panel-layout plane as addressed by lane t of an R-lane group:
+// element y = t + R jj sits at byte offset voff(t, kx) + joff(jj) from the
+// plane base (joff is a compile-time constant per jj: an SGPR or immediate
+// offset of a buffer instruction, so one address VGPR serves the whole line).
+template <int R, int L, int PAN>
+struct PanelLine {
+  static constexpr int PS = panel_stride(R, L, PAN);
+  // element (line, y) of the plane
+  __device__ __forceinline__ static constexpr size_t at(int line, int y) {
+    return (size_t)(y / PAN) * PS + (size_t)line * PAN + y % PAN;
+  }
+  __device__ __forceinline__ static int voff(int t, int kx) {
+    if constexpr (R > PAN) return ((t / PAN) * PS + kx * PAN + t % PAN) * 8;
+    else return (kx * PAN + t) * 8;
+  }
+  __device__ __forceinline__ static constexpr int joff(int jj) {
+    if constexpr (R > PAN) return jj * (R / PAN) * PS * 8;
+    else return (((R * jj) / PAN) * PS + (R * jj) % PAN) * 8;
+  }
+};
+template <int R>
+using LayoutA = PanelLine<R, R * R / 2, pan_a(R)>;
+template <int R>
+using LayoutB = PanelLine<R, R * R, pan_b(R)>;
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// buffer descriptor of a wave-uniform plane (cdna_hip_programming.md T8 recipe)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float2 buf_ld2(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+
+__device__ __forceinline__ void buf_st2(float2 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
+}
 
 // Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
 // the 8 XCDs; placement is a speed hint only, never relied on for
@@ -185,7 +239,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   }
   lds_barrier();
   // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
-  float2* base = ws_a + ((size_t)j * P + pa) * (N / 2) * N;
+  constexpr size_t PLA = plane_a_elems(R);
+  float2* base = ws_a + ((size_t)j * P + pa) * PLA;
   constexpr int CHUNKS = N * GPB / 2;
   static_assert(CHUNKS % NT == 0, "chunking");
 #pragma unroll
@@ -195,134 +250,16 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
     const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
     const float2 a = store_round(tile[tile_pos<R, GPB>(line, r2)]);
     const float2 b = store_round(tile[tile_pos<R, GPB>(line, r2 + 1)]);
-    *reinterpret_cast<float4*>(base + (size_t)line * N + y0 + r2) = make_float4(a.x, a.y, b.x, b.y);
+    const int pl = line / (N / 2);
+    // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
+    *reinterpret_cast<float4*>(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2)) =
+        make_float4(a.x, a.y, b.x, b.y);
   }
 }
 
 // ---------------------------------------------------------------------------
 // Pass 2
 // ---------------------------------------------------------------------------
-// Block = 8 lane groups = LPB lines x 2 roles (the first half of the waves
-// role 1, the rest role 2, so the role is uniform per wave); each group walks
-// ITER lines.  Both roles FFT the same input line (the second read hits
-// L2); role 1 writes B line kx, role 2 the mirrored line:
-//   role 1: G = a1 H(kx),  a1 = Z            (kx != 0)   a1 = (Z + M)/2     (kx == 0)
-//   role 2: G = a2 H(kx),  a2 = M            (kx != 0)   a2 = -i (Z - M)/2, H(N/2, .)  (kx == 0)
-// with Z = F(kx, ky), M = conj F(kx, -ky) (H is even in fx: H(N-kx) = H(kx)).
-template <int R>
-__host__ __device__ constexpr int col_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
-
-template <int R>
-__global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs,
-                                                const float2* __restrict__ ws_a,
-                                                float2* __restrict__ ws_b,
-                                                const float2* __restrict__ htab,
-                                                const float2* __restrict__ tw_glob, int P) {
-  constexpr int N = R * R;
-  constexpr int GPB = 256 / R;          // lane groups per block
-  constexpr int LPB = GPB / 2;          // lines per block per iteration
-  constexpr int ITER = col_iters<R>();
-  constexpr int LB = (N / 2) / (LPB * ITER);
-  static_assert(GPB % 2 == 0 && (64 / R) <= LPB, "role must be wave-uniform");
-  static_assert((N / 2) % (LPB * ITER) == 0, "line blocking");
-  __shared__ float2 tw[N];
-  __shared__ float2 scratch[GPB * R * (R + 1)];
-
-  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
-
-  const int grp = threadIdx.x / R;
-  const int t = threadIdx.x % R;
-  const bool role2 = grp >= LPB;
-  int bid = blockIdx.x;   // (an XCD remap here measured neutral: whole 8-KB lines)
-  const int lb = bid % LB;
-  bid /= LB;
-  const int p = bid % P;
-  const int j = bid / P;
-  const JobDesc jb = jobs[j];
-  if (jb.env < 0) return;
-  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N;
-  float2* bout = ws_b + ((size_t)j * P + p) * N * N;
-  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N;
-  const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
-  const int kx0 = lb * (LPB * ITER) + (grp % LPB);
-
-  float2 nxt[R];
-#pragma unroll
-  for (int jj = 0; jj < R; ++jj) nxt[jj] = ain[(size_t)kx0 * N + t + R * jj];
-  lds_barrier();  // tw visible (the line loads stay in flight)
-
-#pragma unroll 1
-  for (int it = 0; it < ITER; ++it) {
-    const int kx = kx0 + it * LPB;
-    float2 v[R];
-#pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = nxt[jj];
-    const bool dc = (kx == 0);
-    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N;
-#ifdef HBX_EXP_ROLE2_NOLOAD  // timing experiment: only role 1 reads A
-    if (it + 1 < ITER && !role2) {
-#else
-    if (it + 1 < ITER) {  // next line in flight under this line's FFTs
-#endif
-      const float2* in = ain + (size_t)(kx + LPB) * N;
-#pragma unroll
-      for (int jj = 0; jj < R; ++jj) nxt[jj] = in[t + R * jj];
-    }
-    fft_group<R, false>(v, t, sc, tw);
-
-    // F (natural order: lane t, register k2 -> ky = t + R k2) into the scratch,
-    // then M[k2] = conj F(-ky) read back from lane (R - t) mod R, register
-    // R-1-k2 -- for lane 0 its own register (R - k2) mod R, which the extra
-    // pad-slot copy of v[0] turns into one address per lane (+1 offset).
-    // Only the first block iteration of line block 0 can hold kx = 0, so the
-    // general a = alpha Z + beta M form runs there alone (block-uniform
-    // branch); elsewhere role 1 is a = Z (no M at all) and role 2 a = M.
-    const bool general = (lb == 0 && it == 0);
-    if (general || role2) {
-      wave_sync();
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = v[k2];
-      *sc.at(t, R) = v[0];
-      wave_sync();
-    }
-    const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
-    // H(kx, t + R k2) from two bases 4 KB apart: every load then fits the
-    // 12-bit immediate offset (otherwise the compiler keeps per-k2 64-bit
-    // offsets live across the loop and spills them)
-    const float2* hq = hp + t;
-    const float2* hq2 = hq + 16 * R;
-    auto hload = [&](int k2) { return k2 < 16 ? hq[R * k2] : hq2[R * (k2 - 16)]; };
-    if (general) {
-      float2 alpha, beta;
-      if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
-                    beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
-      else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
-                    beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) {
-        const float2 a = cadd(cmul(alpha, v[k2]), cmul(beta, conjf2(mrow[-k2])));
-        v[k2] = cmul(a, hload(k2));
-      }
-    } else if (role2) {
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) v[k2] = cmul(conjf2(mrow[-k2]), hload(k2));
-    } else {
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) {
-#if defined(HBX_EXP_NOH)  // timing experiment: transfer-function loads removed
-        (void)hload;
-#else
-        v[k2] = cmul(v[k2], hload(k2));
-#endif
-      }
-    }
-    fft_group<R, true>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
-    float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N;
-#pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) out[t + R * k2] = v[k2];
-  }
-}
-
 // Column pass, one lane group per input line and both of its output lines:
 // forward FFT over y -> Z; Z into the group's scratch, M = conj Z(-ky) read
 // back into registers; both multiplied by the same H(kx, .) row (H is even
@@ -335,7 +272,11 @@ __global__ __launch_bounds__(256, 2) void k_col(const JobDesc* __restrict__ jobs
 // second inverse FFT.  Scalar-f32 FFTs here: with two lines in registers the
 // packed variant (hbx_fft.hpp) spills.
 #ifndef HBX_COL2_SCALAR
+#ifdef HBX_COL2_PACKED   // A/B switch: `make exp EXP=COL2_PACKED`
+#define HBX_COL2_SCALAR false
+#else
 #define HBX_COL2_SCALAR true
+#endif
 #endif
 #if HBX_COL2_SCALAR
 #define COL2_T float2
@@ -378,21 +319,30 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   const int j = bid / P;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;
-  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N + t;
-  float2* bout = ws_b + ((size_t)j * P + p) * N * N + t;
-  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N + t;
+  using PA = LayoutA<R>;   // A planes: N/2 lines
+  using PB = LayoutB<R>;   // B planes: N lines
+  const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * plane_a_elems(R), plane_a_elems(R) * 8);
+  const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
+  // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
+  const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
   const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
-  const int kx0 = lb * (GPB * ITER) + grp;
+  // the LB blocks of a plane run side by side: at iteration it they hold lines
+  // it * LB * GPB + [0, LB * GPB), i.e. whole contiguous stretches of every panel
+  constexpr int KSTEP = LB * GPB;
+  const int kx0 = lb * GPB + grp;
 
   COL2_T v[R];
+  {
+    const int vo = PA::voff(t, kx0);
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(ain[(size_t)kx0 * N + R * jj]);
+    for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2(ra, vo, PA::joff(jj)));
+  }
   lds_barrier();  // tw visible (the line loads stay in flight)
 
 #pragma unroll 1
   for (int it = 0; it < ITER; ++it) {
-    const int kx = kx0 + it * GPB;
+    const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     fft_group<R, false, HBX_COL2_SCALAR>(v, t, sc, tw);
     // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
@@ -400,14 +350,14 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
     // R-1-k2, or for lane 0 its own register (R - k2) mod R.  Each H value is
     // consumed as it arrives, so H never needs a register array of its own.
-    const float2* hrow = hg + (size_t)kx * N;
+    const int vh = (kx * N + t) * 8;
     wave_sync();
     if (!dc) {
 #pragma unroll
       for (int c8 = 0; c8 < R; c8 += 8) {   // H in batches of 8 loads
         float2 hb[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = hrow[R * (c8 + i)];
+        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * R * 8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int k2 = c8 + i;
@@ -427,128 +377,31 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #pragma unroll
     for (int k2 = 0; k2 < R; ++k2) m[k2] = COL2_LD(conjf2(mrow[-k2]));
     if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
-      const float2* hnyq = hg + (size_t)(N / 2) * N;
+      const int vn = ((N / 2) * N + t) * 8;
 #pragma unroll
       for (int k2 = 0; k2 < R; ++k2) {
         const float2 z = COL2_ST(v[k2]), mm = COL2_ST(m[k2]);
-        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), hrow[R * k2]));
-        m[k2] = COL2_LD(cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), hnyq[R * k2]));
+        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), buf_ld2(rh, vh, k2 * R * 8)));
+        m[k2] = COL2_LD(cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * R * 8)));
       }
     }
     fft_group<R, true, HBX_COL2_SCALAR>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
     {
-      float2* out = bout + (size_t)kx * N;
+      const int vo = PB::voff(t, kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = store_round(COL2_ST(v[k2]));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2(store_round(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
     }
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
-      const float2* in = ain + (size_t)(kx + GPB) * N;
+      const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(in[R * jj]);
+      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2(ra, vo, PA::joff(jj)));
     }
     fft_group<R, true, HBX_COL2_SCALAR>(m, t, sc, tw);
     {
-      float2* out = bout + (size_t)(dc ? N / 2 : N - kx) * N;
+      const int vo = PB::voff(t, dc ? N / 2 : N - kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) out[R * k2] = store_round(COL2_ST(m[k2]));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2(store_round(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
     }
-  }
-}
-
-// N = 1024 column pass on whole-wave FFTs (hbx_fft.hpp): one line per wave,
-// 16 values per lane.  Same two-role scheme as k_col (waves 0, 1 role 1 on lines
-// kx, kx + 1; waves 2, 3 role 2 on the same input lines), but a lane holds a
-// quarter of the registers of the 32-lane version, so the next A line, this
-// line's transfer-function row and the line itself are all in flight at three
-// workgroups (12 waves) per CU: 43 KB of LDS, <= 168 VGPRs.
-// The spectrum stays in slot order (ky = wave_ky_base(L) + 16 m1) between the
-// forward and inverse FFTs; H is read in that order.  M = conj F(-ky) goes
-// through the wave's scratch in natural order, padded every 256 entries.
-__device__ __forceinline__ int mpad(int ky) { return ky + ((ky >> 8) << 3); }
-
-constexpr int kColWaveIter = 4;   // lines per wave
-constexpr int kColWaveLines = 2 * kColWaveIter;   // input lines per workgroup
-
-__global__ __launch_bounds__(256, 3) void k_col_w(const JobDesc* __restrict__ jobs,
-                                                  const float2* __restrict__ ws_a,
-                                                  float2* __restrict__ ws_b,
-                                                  const float2* __restrict__ htab,
-                                                  const float2* __restrict__ tww, int P) {
-  constexpr int N = 1024;
-  constexpr int LB = (N / 2) / kColWaveLines;
-  __shared__ float2 tw1[1024];
-  __shared__ float2 tw2[64];
-  __shared__ __attribute__((aligned(16))) float2 scratch[4 * kWaveScratch];
-  for (int i = threadIdx.x; i < 1024 + 64; i += 256) {
-    if (i < 1024) tw1[i] = tww[i];
-    else tw2[i - 1024] = tww[i];
-  }
-  const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
-  const bool role2 = w >= 2;
-  int bid = blockIdx.x;
-  const int lb = bid % LB;
-  bid /= LB;
-  const int p = bid % P;
-  const int j = bid / P;
-  const JobDesc jb = jobs[j];
-  if (jb.env < 0) return;  // uniform per block
-  const float2* ain = ws_a + ((size_t)j * P + p) * (N / 2) * N;
-  float2* bout = ws_b + ((size_t)j * P + p) * N * N;
-  const float2* hg = htab + (size_t)jb.group * (N / 2 + 1) * N;
-  float2* scr = scratch + w * kWaveScratch;
-  const int kyb = wave_ky_base(L);
-  const int kx0 = lb * kColWaveLines + (w & 1);
-
-  float2 nxt[16];
-#pragma unroll
-  for (int jj = 0; jj < 16; ++jj) nxt[jj] = ain[(size_t)kx0 * N + L + 64 * jj];
-  lds_barrier();  // tables visible (the line loads stay in flight)
-
-  // fully unrolled: nxt and v swap registers instead of being copied (a copy
-  // forces an early wait on the prefetch), and with no loop back-edge the
-  // vmcnt waits are exact (a merge point makes them count the previous line's
-  // stores too)
-#pragma unroll
-  for (int it = 0; it < kColWaveIter; ++it) {
-    const int kx = kx0 + 2 * it;
-    const bool dc = (kx == 0);
-    float2 v[16];
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) v[jj] = nxt[jj];
-    // this line's H row (slot order) lands under the forward FFT
-    const float2* hp = hg + (size_t)((role2 && dc) ? N / 2 : kx) * N + kyb;
-    float2 h[16];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) h[m] = hp[16 * m];
-    {  // next line in flight under both FFTs.  Unconditional (the last
-       // iteration re-reads its own line from L2): a conditional prefetch
-       // makes the H wait below a vmcnt(0) that also waits for this line.
-      const int kn = (it + 1 < kColWaveIter) ? kx + 2 : kx;
-      const float2* in = ain + (size_t)kn * N + L;
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) nxt[jj] = in[64 * jj];
-    }
-    wave_fft1024_fwd(v, L, scr, tw1, tw2);
-
-    wave_sync();
-#pragma unroll
-    for (int m = 0; m < 16; ++m) scr[mpad(kyb + 16 * m)] = v[m];
-    wave_sync();
-    float2 alpha, beta;   // a = alpha Z + beta M (see k_col)
-    if (!role2) { alpha = dc ? make_float2(0.5f, 0.f) : make_float2(1.f, 0.f);
-                  beta = dc ? make_float2(0.5f, 0.f) : make_float2(0.f, 0.f); }
-    else        { alpha = dc ? make_float2(0.f, -0.5f) : make_float2(0.f, 0.f);
-                  beta = dc ? make_float2(0.f, 0.5f) : make_float2(1.f, 0.f); }
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      const float2 mm = scr[mpad((N - (kyb + 16 * m)) & (N - 1))];
-      const float2 a = cadd(cmul(alpha, v[m]), cmul(beta, conjf2(mm)));
-      v[m] = cmul(a, h[m]);
-    }
-    wave_fft1024_inv(v, L, scr, tw1, tw2);   // its first scratch write follows a wave_sync
-    float2* out = bout + (size_t)(role2 ? (dc ? N / 2 : N - kx) : kx) * N + L;
-#pragma unroll
-    for (int jj = 0; jj < 16; ++jj) out[64 * jj] = v[jj];
   }
 }
 
@@ -592,14 +445,15 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
   }
   const int y0 = rb * GPB;
   const int y = y0 + grp;
-  const float2* jbase = ws_b + (size_t)j * P * N * N;
+  constexpr size_t PLB = plane_b_elems(R);
+  const float2* jbase = ws_b + (size_t)j * P * PLB;
 
   float4 pre[PER];   // this thread's share of a plane tile, one plane ahead
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = threadIdx.x + NT * i;
     const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-    pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * N + y0 + r2);
+    pre[i] = *reinterpret_cast<const float4*>(jbase + LayoutB<R>::at(line, y0 + r2));
   }
   float acc[R];
 #pragma unroll
@@ -616,12 +470,12 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
       tile[tile_pos<R, GPB>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
     }
     if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
-      const float2* nb = jbase + (size_t)(p + 1) * N * N;
+      const float2* nb = jbase + (size_t)(p + 1) * PLB;
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int c = threadIdx.x + NT * i;
         const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-        pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * N + y0 + r2);
+        pre[i] = *reinterpret_cast<const float4*>(nb + LayoutB<R>::at(line, y0 + r2));
       }
     }
     lds_barrier();
@@ -829,27 +683,9 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   }
   {
     if (tm) tm->begin(1, st);
-#ifdef HBX_COL_WAVE   // A/B switch: whole-wave FFT column pass at N = 1024
-    if constexpr (N == 1024) {
-#else
-    if constexpr (false) {
-#endif
-      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / kColWaveLines);
-      hipLaunchKernelGGL(k_col_w, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
-                         pd.htab, pd.tw + N, P);
-    } else {
-#ifdef HBX_COL_ROLES   // A/B switch: the two-role column pass
-      constexpr int LINES_PER_BLOCK = (GPB / 2) * col_iters<R>();
-      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
-      hipLaunchKernelGGL(k_col<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
-                         pd.htab, pd.tw, P);
-#else
-      constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
-      const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
-      hipLaunchKernelGGL(k_col2<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
-                         pd.htab, pd.tw, P);
-#endif
-    }
+    constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
+    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
+    hipLaunchKernelGGL(k_col2<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
     if (tm) tm->end(1, n_jobs, st);
   }
   {
