@@ -143,10 +143,21 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     torch.cuda.synchronize()
     dt2 = time.perf_counter() - t0
     plan.close()
+    a1 = np.zeros(n_flips, bool)
+    a2 = np.zeros(n_flips, bool)
+    a1[res.accepted_positions] = True
+    a2[r2.accepted_positions] = True
+    diff = np.nonzero(a1 != a2)[0]
     out["incremental_mode"] = {"flips": r2.steps, "seconds": round(dt2, 3),
                                "flips_per_s": round(r2.steps / dt2, 1), "accepted": len(r2.accepted_positions),
-                               "same_accepts_as_fft_mode": r2.accepted_positions == res.accepted_positions,
-                               "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1)}
+                               "same_accepts_as_fft_mode": bool(len(diff) == 0),
+                               "first_decision_difference": int(diff[0]) if len(diff) else None,
+                               "decisions_differing": int(len(diff)),
+                               "psnr_gain_db": round(r2.final_psnr - r2.initial_psnr, 6),
+                               "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1),
+                               "note": "a flip moves the 1024x24 PSNR by a median 6.5e-7 dB "
+                                       "(profiles/r01_precision_cfg5.json); the two f32 paths can order "
+                                       "near-ties differently, after which the greedy sequences diverge"}
     return out
 
 

@@ -344,20 +344,28 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   for (int it = 0; it < ITER; ++it) {
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
+    const int vh = (kx * N + t) * 8;
+#ifdef HBX_COL2_HEARLY   // A/B switch: the whole H row issued before the forward FFT
+    float2 hall[R];
+#pragma unroll
+    for (int k2 = 0; k2 < R; ++k2) hall[k2] = buf_ld2(rh, vh, k2 * R * 8);
+#define COL2_H(k2) hall[k2]
+#else
+#define COL2_H(k2) buf_ld2(rh, vh, (k2) * R * 8)
+#endif
     fft_group<R, false, HBX_COL2_SCALAR>(v, t, sc, tw);
     // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
     // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
     // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
     // R-1-k2, or for lane 0 its own register (R - k2) mod R.  Each H value is
     // consumed as it arrives, so H never needs a register array of its own.
-    const int vh = (kx * N + t) * 8;
     wave_sync();
     if (!dc) {
 #pragma unroll
       for (int c8 = 0; c8 < R; c8 += 8) {   // H in batches of 8 loads
         float2 hb[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * R * 8);
+        for (int i = 0; i < 8; ++i) hb[i] = COL2_H(c8 + i);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int k2 = c8 + i;
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #pragma unroll
       for (int k2 = 0; k2 < R; ++k2) {
         const float2 z = COL2_ST(v[k2]), mm = COL2_ST(m[k2]);
-        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), buf_ld2(rh, vh, k2 * R * 8)));
+        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), COL2_H(k2)));
         m[k2] = COL2_LD(cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * R * 8)));
       }
     }
@@ -403,6 +411,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       for (int k2 = 0; k2 < R; ++k2) buf_st2(store_round(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
     }
   }
+#undef COL2_H
 }
 
 // ---------------------------------------------------------------------------
