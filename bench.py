@@ -63,11 +63,16 @@ def algorithmic_bytes(N: int, P: int):
     k_rowfwd: read P*N^2/8 mask bits, write P*N^2/2 complex64 (half spectrum)
     k_col:    read P*N^2/2 complex64, write P*N^2 complex64
     k_rowinv: read P*N^2 complex64 + N^2 f32 target
+    k_bits_t:  (bits -> column pipeline, N = 1024) read P*N^2/8 mask bits, write P*N^2/4
+               nibble codes of the transposed bits
+    k_colbits: read the P*N^2/4 codes, write P*N^2 complex64 (no row-spectrum intermediate)
     k_psf_eval:   read the touched plane's field (8 N^2) + group intensity (4 N^2) + target (4 N^2)
     k_psf_commit: accepted envs only: read + write field and intensity (24 N^2)."""
     return {"k_rowfwd": P * N * N // 8 + P * N * N * 4,
             "k_col": P * N * N * 4 + P * N * N * 8,
             "k_rowinv": P * N * N * 8 + N * N * 4,
+            "k_bits_t": P * N * N // 8 + P * N * N // 4,
+            "k_colbits": P * N * N // 4 + P * N * N * 8,
             "k_psf_eval": 16 * N * N,
             "k_psf_commit": 24 * N * N}
 
@@ -324,7 +329,8 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
-        step_bytes = (abytes["k_rowfwd"] + abytes["k_col"] + abytes["k_rowinv"]) * B
+        step_bytes = sum(abytes[k] for k in timing if k in ("k_rowfwd", "k_col", "k_rowinv", "k_bits_t",
+                                                             "k_colbits")) * B
         canon = canonical_step_bytes(N, P)
         out = {
             "metric": "env-steps/sec (1024x1024, 24-plane)",

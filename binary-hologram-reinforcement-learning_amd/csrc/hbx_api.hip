@@ -156,6 +156,33 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
         tw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
       }
   }
+  if (N == 1024) {  // class tables of the bits -> column pass (hbx_internal.hpp kTwClassOff)
+    tw.resize((size_t)hbx::kTwClassOff + 33 * (size_t)hbx::kTwClassStride, make_float2(0.f, 0.f));
+    for (int c = 0; c <= 32; ++c) {
+      float2* ct = tw.data() + hbx::kTwClassOff + (size_t)c * hbx::kTwClassStride;
+      const int k1 = c % 32;
+      for (int k = 0; k < 8; ++k)
+        for (int v = 0; v < 16; ++v) {
+          double re = 0.0, im = 0.0;
+          for (int jb = 0; jb < 4; ++jb)
+            if ((v >> jb) & 1) {
+              const double a = -2.0 * M_PI * (double)((k1 * (4 * k + jb)) % 32) / 32.0;
+              re += std::cos(a);
+              im += std::sin(a);
+            }
+          ct[k * 16 + v] = make_float2((float)re, (float)im);
+        }
+      for (int n2 = 0; n2 < 16; ++n2) {
+        const double a = -2.0 * M_PI * (double)((c * n2) % 1024) / 1024.0;
+        ct[128 + n2] = make_float2((float)std::cos(a), (float)std::sin(a));
+      }
+      const double a = -2.0 * M_PI * (double)(c % 64) / 64.0;
+      ct[144] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    // opt-in A/B switch: measured slower than the three-pass path (colbits)
+    const char* ev = std::getenv("HBX_COLBITS");
+    pd.colbits = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
+  }
   const size_t hrow = (size_t)(N / 2 + 1) * N;
   std::vector<float2> ht((size_t)G * hrow);
   const double scale = 1.0 / ((double)N * (double)N);  // ifft2 normalisation
@@ -232,6 +259,13 @@ int hbx_plan_destroy(hbx_plan_t p) {
 }
 
 size_t hbx_plan_workspace_bytes(hbx_plan_t p) { return p ? p->ws_bytes : 0; }
+
+int hbx_plan_pipeline(hbx_plan_t p) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (p->pd.R == 0) return HBX_PIPE_GENERIC;
+  return (p->pd.R == 32 && p->pd.colbits) ? HBX_PIPE_COLBITS : HBX_PIPE_THREE_PASS;
+}
 
 }  // extern "C"
 

@@ -50,6 +50,27 @@ __host__ __device__ constexpr size_t plane_b_elems(int R) {
   return (size_t)(R * R / pan_b(R)) * panel_stride(R, R * R, pan_b(R));
 }
 
+// Line kx of a panel-layout plane as addressed by lane t of an R-lane group:
+// element y = t + R jj sits at byte offset voff(t, kx) + joff(jj) from the
+// plane base (joff is a compile-time constant per jj: an SGPR or immediate
+// offset of a buffer instruction, so one address VGPR serves the whole line).
+template <int R, int L, int PAN>
+struct PanelLine {
+  static constexpr int PS = panel_stride(R, L, PAN);
+  // element (line, y) of the plane
+  __device__ __forceinline__ static constexpr size_t at(int line, int y) {
+    return (size_t)(y / PAN) * PS + (size_t)line * PAN + y % PAN;
+  }
+  __device__ __forceinline__ static int voff(int t, int kx) {
+    if constexpr (R > PAN) return ((t / PAN) * PS + kx * PAN + t % PAN) * 8;
+    else return (kx * PAN + t) * 8;
+  }
+  __device__ __forceinline__ static constexpr int joff(int jj) {
+    if constexpr (R > PAN) return jj * (R / PAN) * PS * 8;
+    else return (((R * jj) / PAN) * PS + (R * jj) % PAN) * 8;
+  }
+};
+
 // Optional hipEvent pairs around every pass launch (hbx_plan_set_timing).
 constexpr int kNumPasses = 5;  // rowfwd, col, rowinv, psf_eval, psf_commit
 struct PassTimer {
@@ -84,10 +105,19 @@ struct PlanDev {
   double* psf_partial; // [max_jobs][kPsfBlocks][2]
   int32_t* psf_order;  // [max_jobs] jobs sorted by colour group (launch order)
   float* zero_row;     // [N] zeros: the target row of a propagation without a target
+  int colbits;         // N = 1024: bits -> column pass without the A intermediate (hbx_colbits.hip)
   PassTimer* timer;    // nullable
 };
 
 constexpr int kPsfBlocks = 64;   // blocks per job of the incremental-field kernels
+
+// N = 1024 class tables appended to PlanDev::tw (hbx_colbits.hip): class c = 0..32 at
+// kTwClassOff + c * kTwClassStride: [8][16] nibble tables sum_j v_j W32^{(c mod 32)(4k + j)},
+// [16] W1024^{c n2}, [1] W64^c
+constexpr int kTwClassOff = 1024 + 16 * 64 + 16 * 4;
+constexpr int kTwClassStride = 160;
+hipError_t launch_colbits(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
+                          hipStream_t st);
 
 struct EnvDev {
   uint64_t* mask;

@@ -86,26 +86,6 @@ constexpr int kRowNT = row_nt(R);
 template <int R>
 constexpr int kPanel = panel_rows(R);
 
-// Line kx of a panel-layout plane as addressed by lane t of an R-lane group:
-// element y = t + R jj sits at byte offset voff(t, kx) + joff(jj) from the
-// plane base (joff is a compile-time constant per jj: an SGPR or immediate
-// offset of a buffer instruction, so one address VGPR serves the whole line).
-template <int R, int L, int PAN>
-struct PanelLine {
-  static constexpr int PS = panel_stride(R, L, PAN);
-  // element (line, y) of the plane
-  __device__ __forceinline__ static constexpr size_t at(int line, int y) {
-    return (size_t)(y / PAN) * PS + (size_t)line * PAN + y % PAN;
-  }
-  __device__ __forceinline__ static int voff(int t, int kx) {
-    if constexpr (R > PAN) return ((t / PAN) * PS + kx * PAN + t % PAN) * 8;
-    else return (kx * PAN + t) * 8;
-  }
-  __device__ __forceinline__ static constexpr int joff(int jj) {
-    if constexpr (R > PAN) return jj * (R / PAN) * PS * 8;
-    else return (((R * jj) / PAN) * PS + (R * jj) % PAN) * 8;
-  }
-};
 template <int R>
 using LayoutA = PanelLine<R, R * R / 2, pan_a(R)>;
 template <int R>
@@ -683,6 +663,10 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   const int P = pd.P;
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
+  if (R == 32 && pd.colbits) {   // bits -> B without the A intermediate (hbx_colbits.hip)
+    const hipError_t e = launch_colbits(pd, jobs, n_jobs, mask, st);
+    if (e != hipSuccess) return e;
+  } else {
   {
     const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R));
     if (tm) tm->begin(0, st);
@@ -696,6 +680,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
     hipLaunchKernelGGL(k_col2<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
     if (tm) tm->end(1, n_jobs, st);
+  }
   }
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 3
+ABI_VERSION = 4
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -25,13 +25,18 @@ MAX_GROUPS = 4
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
-    "hbx_plan_workspace_bytes", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
+    "hbx_plan_workspace_bytes", "hbx_plan_pipeline", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
     "hbx_eval_flips_psf", "hbx_commit_flip_psf",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
+# kernels in the ROWFWD / COL timer slots per pipeline (hbx_plan_pipeline)
+PIPE_THREE_PASS, PIPE_COLBITS, PIPE_GENERIC = 0, 1, 2
+PIPE_PASS_NAMES = {PIPE_THREE_PASS: PASS_NAMES,
+                   PIPE_COLBITS: ("k_bits_t", "k_colbits", "k_rowinv", "k_psf_eval", "k_psf_commit"),
+                   PIPE_GENERIC: PASS_NAMES}
 
 
 class HbxError(RuntimeError):
@@ -82,6 +87,7 @@ def _declare(lib):
     lib.hbx_plan_destroy.argtypes = [VP]
     lib.hbx_plan_workspace_bytes.argtypes = [VP]
     lib.hbx_plan_workspace_bytes.restype = C.c_size_t
+    lib.hbx_plan_pipeline.argtypes = [VP]
     lib.hbx_propagate.argtypes = [VP, VP, VP, I32, VP, VP, VP, VP]
     lib.hbx_psnr.argtypes = [VP, VP, I32, VP, VP]
     lib.hbx_env_reset.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, VP]

@@ -175,7 +175,16 @@ class Plan:
         n = (C.c_int64 * _lib.NUM_PASSES)()
         jobs = (C.c_int64 * _lib.NUM_PASSES)()
         _lib.check(self.lib.hbx_plan_read_timing(self._h, ms, n, jobs), "hbx_plan_read_timing")
-        return {name: (ms[i], n[i], jobs[i]) for i, name in enumerate(_lib.PASS_NAMES)}
+        names = _lib.PIPE_PASS_NAMES[self.pipeline]
+        return {name: (ms[i], n[i], jobs[i]) for i, name in enumerate(names)}
+
+    @property
+    def pipeline(self) -> int:
+        """hbx_plan_pipeline: _lib.PIPE_THREE_PASS / PIPE_COLBITS / PIPE_GENERIC."""
+        rc = int(self.lib.hbx_plan_pipeline(self._h))
+        if rc < 0:
+            _lib.check(rc, "hbx_plan_pipeline")
+        return rc
 
     # -- buffer helpers -------------------------------------------------------
     def mask_shape(self, n_env: int):

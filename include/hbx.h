@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 3
+#define HBX_ABI_VERSION 4
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -127,6 +127,17 @@ int hbx_plan_create(hbx_plan_t* plan, const hbx_optics_t* optics, int32_t max_jo
                     int32_t device);
 int hbx_plan_destroy(hbx_plan_t plan);
 size_t hbx_plan_workspace_bytes(hbx_plan_t plan);
+/* Propagation pipeline the plan runs (ABI v4): which kernels fill the pass
+ * timer slots HBX_PASS_ROWFWD / HBX_PASS_COL below.
+ *   HBX_PIPE_THREE_PASS  k_rowfwd -> k_col2 -> k_rowinv (N = 64, 256, 1024; the default)
+ *   HBX_PIPE_COLBITS     N = 1024 with HBX_COLBITS=1 in the environment at plan creation:
+ *                        k_bits_t -> k_colbits -> k_rowinv (no row-spectrum intermediate;
+ *                        slots ROWFWD / COL time k_bits_t / k_colbits; measured slower)
+ *   HBX_PIPE_GENERIC     N = 896: composed mixed-radix path */
+#define HBX_PIPE_THREE_PASS 0
+#define HBX_PIPE_COLBITS 1
+#define HBX_PIPE_GENERIC 2
+int hbx_plan_pipeline(hbx_plan_t plan);
 
 /* Full propagation of every group of n_env masks (env.py:123-133 reset path,
  * env_1024_24.py:149-166, DBS_1024_24.py:244-257):

@@ -163,6 +163,74 @@ def test_eval_flips_1024_vs_oracle():
     assert np.max(np.abs(got.cpu().numpy() - np.array(want))) <= PSNR_TOL
 
 
+def _plan_path(cfg, max_jobs, legacy):
+    """Plan on the three-pass path (default) or the bits -> column path (HBX_COLBITS=1)."""
+    import hbx
+    old = os.environ.pop("HBX_COLBITS", None)
+    try:
+        if not legacy:
+            os.environ["HBX_COLBITS"] = "1"
+        plan = hbx.Plan(cfg, max_jobs=max_jobs)
+        assert plan.pipeline == (hbx._lib.PIPE_THREE_PASS if legacy else hbx._lib.PIPE_COLBITS)
+        return plan
+    finally:
+        os.environ.pop("HBX_COLBITS", None)
+        if old is not None:
+            os.environ["HBX_COLBITS"] = old
+
+
+@pytest.mark.parametrize("field_kind", [0, 1])   # amplitude {0,1}, binary phase {+1,-1}
+def test_colbits_matches_three_pass_1024(field_kind):
+    """N = 1024: the bits -> column pass (hbx_colbits.hip) against the three-pass
+    path on 8 envs (24 jobs: the XCD job mapping) with flips on every row class:
+    stats rtol 2e-6, intensity 2e-6 * max; and the legacy path itself vs the oracle."""
+    import hbx
+    cfg = hbx.rgb_config(1024, field_kind=field_kind)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    pre = torch.rand((8, 24, 1024, 1024), generator=g, device="cuda")
+    bits = hbx.pack_bits(pre >= 0.5)
+    tgt = torch.rand((8, 3, 1024, 1024), generator=g, device="cuda")
+    new = _plan_path(cfg, 24, legacy=False)
+    old = _plan_path(cfg, 24, legacy=True)
+    a = new.propagate(bits, tgt)
+    b = old.propagate(bits, tgt)
+    torch.cuda.synchronize()
+    assert torch.allclose(a[1], b[1], rtol=2e-6, atol=0)
+    assert float((a[0] - b[0]).abs().max()) <= 2e-6 * float(b[0].abs().max())
+    assert float((a[2] - b[2]).abs().max()) <= 1e-5
+    # flips: every colour plane, rows / columns at the class boundaries (x mod 64 = 0, 31, 32, 63)
+    n = 1024 * 1024
+    fl = [c * n + r * 1024 + x for c in (0, 5, 8, 15, 16, 23) for (r, x) in
+          ((0, 0), (1023, 1023), (511, 31), (512, 32), (7, 63), (300, 64 * 7 + 33))]
+    flips = torch.tensor(fl, dtype=torch.int64, device="cuda")
+    st0 = a[1][0].contiguous()
+    pa, _ = new.eval_flips(bits[0], tgt[0], st0, flips)
+    pb, _ = old.eval_flips(bits[0], tgt[0], st0, flips)
+    torch.cuda.synchronize()
+    assert float((pa - pb).abs().max()) <= 2e-5
+
+
+def test_colbits_1024_vs_oracle_flips():
+    """The bits -> column path against the float64 oracle: full propagation and 8 flips
+    (K = 8 jobs, XCD mapping), amplitude field."""
+    import hbx
+    ocfg = O.rgb_config(1024)
+    pre, tgt = O.synthetic_inputs(ocfg, 4)
+    env = O.OracleEnv(ocfg)
+    env.reset(pre, tgt)
+    n = 1024 * 1024
+    flips = np.array([0, n - 1, 3 * n + 64 * 5, 9 * n + 5 * 1024 + 77, 12 * n + 1023 * 1024 + 32,
+                      17 * n + 512 * 1024 + 511, 20 * n + 33, 24 * n - 1], np.int64)
+    want = [env.evaluate_flip(int(f))[0] for f in flips]
+    plan = _plan_path(dev_cfg(ocfg), 8, legacy=False)
+    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    _, st, ps = plan.propagate(bits[None], torch.from_numpy(tgt).cuda()[None])
+    assert abs(float(ps[0]) - env.initial_psnr) <= PSNR_TOL
+    got, _ = plan.eval_flips(bits, torch.from_numpy(tgt).cuda(), st[0].contiguous(),
+                             torch.from_numpy(flips).cuda())
+    assert np.max(np.abs(got.cpu().numpy() - np.array(want))) <= PSNR_TOL
+
+
 # -- env semantics ---------------------------------------------------------------------------
 def test_env_trace_golden(golden_dir):
     import hbx
