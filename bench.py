@@ -147,6 +147,13 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     r2 = dbs.greedy(plan, m2, target, order, mode="psf")
     torch.cuda.synchronize()
     dt2 = time.perf_counter() - t0
+    m3 = mask.clone()
+    dbs.greedy(plan, m3.clone(), target, order[:256], mode="psf_host")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r3 = dbs.greedy(plan, m3, target, order, mode="psf_host")
+    torch.cuda.synchronize()
+    dt3 = time.perf_counter() - t0
     plan.close()
     a1 = np.zeros(n_flips, bool)
     a2 = np.zeros(n_flips, bool)
@@ -160,6 +167,14 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                                "decisions_differing": int(len(diff)),
                                "psnr_gain_db": round(r2.final_psnr - r2.initial_psnr, 6),
                                "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1),
+                               "batches": r2.launches,
+                               "walk": "device-resident (hbx_dbs_walk_psf): eval, one-block decide and commit launches per batch, "
+                                       "one host sync per 64 batches",
+                               "host_decided_batches": {
+                                   "flips_per_s": round(r3.steps / dt3, 1), "seconds": round(dt3, 3),
+                                   "batches": r3.launches,
+                                   "same_accepts_as_device_walk": r3.accepted_positions == r2.accepted_positions,
+                                   "note": "hbx_eval_flips_psf + host decision + hbx_commit_flip_psf per batch"},
                                "note": "a flip moves the 1024x24 PSNR by a median 6.5e-7 dB "
                                        "(profiles/r01_precision_cfg5.json); the two f32 paths can order "
                                        "near-ties differently, after which the greedy sequences diverge"}

@@ -62,6 +62,8 @@ struct hbx_plan {
   float2* map_x = nullptr;       // [4P + P/2 + 1][N][N]
   float2* map_s = nullptr;       // same size: FFT scratch
   float2* map_y = nullptr;       // [P + P/2 + 1][N][N]
+  double* walk_partial = nullptr;  // [kWalkMaxK x blocks][2] (lazy, hbx_dbs_walk_psf)
+  size_t walk_partial_elems = 0;
 };
 
 namespace {
@@ -248,6 +250,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->delta) (void)hipFree(p->delta);
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
+  if (p->walk_partial) (void)hipFree(p->walk_partial);
   if (p->pd.psf_order) (void)hipFree(p->pd.psf_order);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
@@ -754,6 +757,53 @@ int hbx_commit_flip_psf(hbx_plan_t p, uint64_t* base_mask, double* base_chan_sta
   // psf_order is already {0}: launch_psf_commit visits the single job
   HBX_HIP(hbx::launch_psf_commit(pd, p->jobs, 1, base_mask, reinterpret_cast<float2*>(field), intensity,
                                  p->accept_flag, st));
+  return HBX_OK;
+}
+
+int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, double* base_chan_stats,
+                     float* field, float* intensity, const int64_t* order, hbx_dbs_walk_t* walk,
+                     int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int32_t K,
+                     int32_t batches, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !target || !base_chan_stats || !field || !intensity || !order || !walk)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (accept_cap < 0 || (accept_cap > 0 && (!accept_pos || !accept_psnr)))
+    return fail(HBX_ERR_INVALID, "accept log");
+  if (K < 1 || K > hbx::kWalkMaxK) return fail(HBX_ERR_INVALID, "K must be in [1, 256]");
+  if (batches < 0) return fail(HBX_ERR_INVALID, "batches");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  rc = ensure_hpsf(p, st);
+  if (rc) return rc;
+  const PlanDev& pd = p->pd;
+  const size_t need = (size_t)K * hbx::walk_blocks_per_job(pd.N, K) * 2;
+  if (need > p->walk_partial_elems) {   // allocation: first call per K range, outside capture
+    if (p->walk_partial) (void)hipFree(p->walk_partial);
+    p->walk_partial = nullptr;
+    p->walk_partial_elems = 0;
+    if (hipMalloc(&p->walk_partial, need * sizeof(double)) != hipSuccess)
+      return fail(HBX_ERR_NOMEM, "walk partials");
+    p->walk_partial_elems = need;
+  }
+  hbx::WalkLaunch l;
+  l.mask = base_mask;
+  l.target = target;
+  l.base_stats = base_chan_stats;
+  l.field = reinterpret_cast<float2*>(field);
+  l.inten = intensity;
+  l.order = order;
+  l.walk = walk;
+  l.log_pos = accept_pos;
+  l.log_psnr = accept_psnr;
+  l.log_cap = accept_cap;
+  l.partial = p->walk_partial;
+  l.K = K;
+  l.batches = batches;
+  l.count = pixel_count(p);
+  l.peak = p->optics.peak;
+  l.rel = p->optics.rel_scale;
+  HBX_HIP(hbx::launch_walk(pd, l, st));
   return HBX_OK;
 }
 

@@ -1,10 +1,24 @@
 // hbx_internal.hpp -- types shared by the kernels and the C-ABI layer.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stddef.h>
 #include <stdint.h>
 
+#include "hbx.h"
+
 namespace hbx {
+
+// tt.relativeLoss(.., tm.get_PSNR) from the channel sums (env.py:174):
+// lsq scale s = sum IT / sum I^2, mse = mean((s I - T)^2), psnr = 10 log10(peak^2 / mse)
+__device__ __forceinline__ double psnr_from(double sxy, double sxx, double syy, double count,
+                                            int rel_scale, double peak) {
+  double mse;
+  if (rel_scale == 1) mse = (sxx > 0.0) ? (syy - sxy * sxy / sxx) / count : syy / count;
+  else mse = (sxx - 2.0 * sxy + syy) / count;
+  if (!(mse > 0.0)) return INFINITY;
+  return 10.0 * log10(peak * peak / mse);
+}
 
 // One colour-group propagation: env index (plan-local), group, optional flip.
 struct JobDesc {
@@ -168,6 +182,26 @@ hipError_t map_group(const PlanDev& pd, int g, const float2* field, const float*
 hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                            const float2* field, const float* inten, const float* target,
                            const double* chan_stats, hipStream_t st);
+// device-resident greedy DBS walk (hbx_walk.hip)
+struct WalkLaunch {
+  uint64_t* mask;
+  const float* target;
+  double* base_stats;
+  float2* field;
+  float* inten;
+  const int64_t* order;
+  hbx_dbs_walk_t* walk;
+  int64_t* log_pos;
+  double* log_psnr;
+  int64_t log_cap;
+  double* partial;   // [K][walk_blocks_per_job(N, K)][2]
+  int K, batches;
+  double count, peak;
+  int rel;
+};
+constexpr int kWalkMaxK = 256;
+int walk_blocks_per_job(int N, int K);
+hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st);
 hipError_t launch_psf_commit(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                              float2* field, float* inten, const int32_t* accept_flag, hipStream_t st);
 hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W, int P, int CH,

@@ -15,15 +15,6 @@ namespace hbx {
 // ---------------------------------------------------------------------------
 // Small per-job / per-env kernels
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double psnr_from(double sxy, double sxx, double syy, double count,
-                                            int rel_scale, double peak) {
-  double mse;
-  if (rel_scale == 1) mse = (sxx > 0.0) ? (syy - sxy * sxy / sxx) / count : syy / count;
-  else mse = (sxx - 2.0 * sxy + syy) / count;
-  if (!(mse > 0.0)) return INFINITY;
-  return 10.0 * log10(peak * peak / mse);
-}
-
 // jobs from actions: one job per env (env.py:157-161 decode)
 __global__ void k_jobs_from_actions(const int64_t* __restrict__ actions, int n, int H, int W,
                                     int P, int CH, JobDesc* __restrict__ jobs,

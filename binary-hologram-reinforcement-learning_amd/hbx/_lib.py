@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 4
+ABI_VERSION = 5
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -22,13 +22,14 @@ REL_NONE, REL_LSQ = 0, 1
 ACCEPT_ENV, ACCEPT_DBS = 0, 1
 REWARD_PSNR, REWARD_IMPORTANCE = 0, 1
 MAX_GROUPS = 4
+WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
     "hbx_plan_workspace_bytes", "hbx_plan_pipeline", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
-    "hbx_eval_flips_psf", "hbx_commit_flip_psf",
+    "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -52,6 +53,18 @@ class Optics(C.Structure):
         ("dx", C.c_double), ("dy", C.c_double), ("z", C.c_double),
         ("tf_kind", C.c_int32), ("field_kind", C.c_int32), ("rel_scale", C.c_int32),
         ("reserved", C.c_int32), ("peak", C.c_double),
+    ]
+
+
+class DbsWalk(C.Structure):
+    """hbx_dbs_walk_t (include/hbx.h): device-resident greedy DBS walk state."""
+    _fields_ = [
+        ("pos", C.c_int64), ("total", C.c_int64), ("accepted", C.c_int64), ("batches", C.c_int64),
+        ("prev_psnr", C.c_double), ("init_psnr", C.c_double), ("last_psnr", C.c_double),
+        ("stop_diff", C.c_double),
+        ("stop_enabled", C.c_int32), ("refresh_every", C.c_int32), ("done", C.c_int32), ("halt", C.c_int32),
+        ("stopped_early", C.c_int32), ("commit_ch", C.c_int32), ("commit_pix", C.c_int32),
+        ("reserved", C.c_int32 * 3),
     ]
 
 
@@ -103,6 +116,7 @@ def _declare(lib):
     lib.hbx_flip_map.argtypes = [VP, VP, VP, VP, VP, VP]
     lib.hbx_eval_flips_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, I32, VP, VP, VP]
     lib.hbx_commit_flip_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]
+    lib.hbx_dbs_walk_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, C.c_int64, I32, I32, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]

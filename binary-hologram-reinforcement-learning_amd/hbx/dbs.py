@@ -3,18 +3,23 @@
 greedy()  -- DBS.py:247-294 / DBS_1024_24.py:313-422: visit pixels in a
              shuffled order, keep a flip iff PSNR strictly improves.  Run as
              SPECULATIVE batches: the next K candidates are evaluated against
-             the current base in one hbx_eval_flips launch; the first improving
-             one (in visiting order) is committed on the device and the walk
-             resumes right after it.  Every candidate before it was evaluated
-             against exactly the state the serial loop would have had, so the
-             accept sequence is the serial one.
+             the current base in one launch; the first improving one (in
+             visiting order) is committed on the device and the walk resumes
+             right after it.  Every candidate before it was evaluated against
+             exactly the state the serial loop would have had, so the accept
+             sequence is the serial one.  mode="psf" runs the whole walk on the
+             device (hbx_dbs_walk_psf: a one-block kernel makes the
+             decision, no host round trip per batch); mode="psf_host" and
+             mode="fft" return to the host after every batch.
 probe()   -- DBS_1024_24-128.py:310-373 / range.py:294-335: every flip
              evaluated against the FIXED base and undone; embarrassingly
              parallel, one launch per max_jobs candidates.
 """
 from __future__ import annotations
 
+import ctypes as C
 import io
+import math
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -22,6 +27,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from . import _lib
 from .plan import Plan
 
 OUTPUT_BINS = np.round(np.linspace(0, 1.0, 11), decimals=10)   # DBS_1024_24.py:209
@@ -62,18 +68,152 @@ def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
     return int(idx[0]) if idx.size else None
 
 
+def walk_k(q: float, n: int, k_min: int = 1, k_max: int = 256) -> int:
+    """Speculation depth of the device walk for acceptance rate q at side n:
+    the K minimising (per-batch overhead + K * per-candidate stream time) /
+    expected candidates consumed per batch, (1 - (1 - q)^K) / q."""
+    o = 12.0                          # us: two launches + the last block's decision
+    c = 16.0 * n * n / 5.0e6          # us: one candidate's 16 B/px at ~5 TB/s
+    q = min(max(q, 1e-6), 1.0)
+    best, bk = math.inf, k_min
+    for k in range(max(1, k_min), max(k_min, k_max) + 1):
+        vis = (1.0 - (1.0 - q) ** k) / q
+        cost = (o + k * c) / vis
+        if cost < best:
+            best, bk = cost, k
+    return bk
+
+
+def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream,
+                 refresh_every, chunk: int = 64) -> GreedyResult:
+    """greedy(mode="psf") on the device-resident walk (hbx_dbs_walk_psf).
+
+    The host keeps two chunks of `chunk` batches in flight: chunk n+1 is
+    enqueued before chunk n's state (copied to pinned memory behind it) is
+    read, so the device never idles on the host; batches enqueued after the
+    walk is done or halted return at once."""
+    dev = plan.device
+    c = plan.cfg
+    s = stream if stream is not None else torch.cuda.current_stream()
+    _, stats, psnr0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                     stream=stream)
+    base_stats = stats[0].contiguous()
+    fc, it = plan.simulate(mask.unsqueeze(0), want_intensity=True, stream=stream)
+    field = torch.view_as_real(fc[0]).contiguous()
+    inten = it[0].contiguous()
+    init = float(psnr0.item())
+    w = _lib.DbsWalk()
+    w.total = total
+    w.prev_psnr = w.init_psnr = init
+    w.last_psnr = math.nan
+    w.stop_enabled = 1 if stop_diff is not None else 0
+    w.stop_diff = float(stop_diff) if stop_diff is not None else 0.0
+    w.refresh_every = int(refresh_every or 0)
+    w.commit_ch = -1
+    nbytes = C.sizeof(_lib.DbsWalk)
+    wbuf = torch.frombuffer(bytearray(bytes(w)), dtype=torch.uint8).to(dev)
+    cap = max(1, total)
+    log_pos = torch.empty(cap, dtype=torch.int64, device=dev)
+    log_psnr = torch.empty(cap, dtype=torch.float64, device=dev)
+    pinned = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    events = [torch.cuda.Event(), torch.cuda.Event()]
+    k_lo, k_hi = max(1, k_min), min(k_max, _lib.WALK_MAX_K)
+    q, pos_prev, acc_prev = 0.5, 0, 0
+    k = walk_k(q, c.height, k_lo, k_hi)
+    marks = []                    # (accepts so far, seconds) per processed chunk
+    exact = {}                    # accept index -> exact PSNR after a refresh
+    issued = done_n = 0
+    t0 = time.perf_counter()
+
+    def issue():
+        nonlocal issued
+        slot = issued % 2
+        plan.dbs_walk_psf(mask, target, base_stats, field, inten, order_t, wbuf, log_pos, log_psnr, k, chunk,
+                          stream=s)
+        with torch.cuda.stream(s):
+            pinned[slot].copy_(wbuf, non_blocking=True)
+        events[slot].record(s)
+        issued += 1
+
+    def take():
+        nonlocal done_n
+        slot = done_n % 2
+        events[slot].synchronize()
+        done_n += 1
+        return _lib.DbsWalk.from_buffer_copy(pinned[slot].numpy().tobytes())
+
+    issue()
+    issue()
+    while True:
+        st = take()
+        marks.append((int(st.accepted), time.perf_counter() - t0))
+        dpos, dacc = st.pos - pos_prev, st.accepted - acc_prev
+        if dpos > 0:
+            q = 0.5 * q + 0.5 * (dacc / dpos)
+            k = walk_k(q, c.height, k_lo, k_hi)
+        pos_prev, acc_prev = st.pos, st.accepted
+        if st.halt:
+            while done_n < issued:        # the chunk behind it saw halt: no-ops
+                st = take()
+            # exact re-propagation bounds the fp32 drift of the incremental updates
+            _, stats, ps_exact = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                                stream=s)
+            base_stats.copy_(stats[0])
+            fc, it = plan.simulate(mask.unsqueeze(0), want_intensity=True, stream=s)
+            field.copy_(torch.view_as_real(fc[0]))
+            inten.copy_(it[0])
+            st.prev_psnr = float(ps_exact.item())
+            st.halt = 0
+            exact[int(st.accepted) - 1] = st.prev_psnr
+            wbuf.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8))
+            if st.done:
+                break
+            issue()
+            issue()
+            continue
+        if st.done:
+            while done_n < issued:
+                take()
+            break
+        issue()
+    seconds = time.perf_counter() - t0
+    n_acc = min(int(st.accepted), cap)
+    acc_pos = log_pos[:n_acc].cpu().tolist()
+    acc_psnr = log_psnr[:n_acc].cpu().tolist()
+    for i, v in exact.items():
+        if i < n_acc:
+            acc_psnr[i] = v
+    acc_t, m = [], 0
+    for i in range(n_acc):                # time of the chunk that logged accept i
+        while m < len(marks) - 1 and marks[m][0] <= i:
+            m += 1
+        acc_t.append(marks[m][1] if marks else seconds)
+    final = acc_psnr[-1] if acc_psnr else init
+    last = None if math.isnan(st.last_psnr) else float(st.last_psnr)
+    return GreedyResult(init, final, int(st.pos), acc_pos, acc_psnr, int(st.batches), bool(st.stopped_early),
+                        acc_t, last, seconds)
+
+
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
            stream=None, mode: str = "fft", refresh_every: int = 4096) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
     mode="fft": every candidate is a full propagation of its colour group.
-    mode="psf": candidates are evaluated on the incremental-field path
-    (hbx_eval_flips_psf: one streaming pass over one plane); the base fields
-    are re-propagated exactly every ``refresh_every`` accepted flips."""
-    if mode not in ("fft", "psf"):
-        raise ValueError(f"mode must be 'fft' or 'psf', got {mode!r}")
+    mode="psf": candidates are evaluated on the incremental-field path, the
+    whole walk device-resident (hbx_dbs_walk_psf); the base fields are
+    re-propagated exactly every ``refresh_every`` accepted flips.
+    mode="psf_host": the same candidates through hbx_eval_flips_psf /
+    hbx_commit_flip_psf with a host decision per batch."""
+    if mode not in ("fft", "psf", "psf_host"):
+        raise ValueError(f"mode must be 'fft', 'psf' or 'psf_host', got {mode!r}")
     dev = plan.device
+    if mode == "psf":
+        order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
+        total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
+        return _greedy_walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
+                            stream, refresh_every)
+    mode = "psf" if mode == "psf_host" else mode
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
     total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)

@@ -294,6 +294,27 @@ class Plan:
                                                 _ptr(group_stats), _ptr(k_dev), _stream(stream)),
                    "hbx_commit_flip_psf")
 
+    def dbs_walk_psf(self, base_mask, target, base_stats, field, intensity, order: torch.Tensor,
+                     walk: torch.Tensor, accept_pos: torch.Tensor, accept_psnr: torch.Tensor, K: int,
+                     batches: int, stream=None):
+        """hbx_dbs_walk_psf: enqueue `batches` speculative batches of K candidates of the
+        device-resident greedy walk.  walk: uint8 [sizeof(hbx_dbs_walk_t)] on the device."""
+        c = self.cfg
+        _need(field, "field", torch.float32, (c.channels, c.height, c.width, 2), self.device)
+        _need(intensity, "intensity", torch.float32, (c.groups, c.height, c.width), self.device)
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
+        _need(order, "order", torch.int64, (order.shape[0],), self.device)
+        _need(walk, "walk", torch.uint8, (C.sizeof(_lib.DbsWalk),), self.device)
+        cap = accept_pos.shape[0]
+        _need(accept_pos, "accept_pos", torch.int64, (cap,), self.device)
+        _need(accept_psnr, "accept_psnr", torch.float64, (cap,), self.device)
+        _lib.check(self.lib.hbx_dbs_walk_psf(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                             _ptr(field), _ptr(intensity), _ptr(order), _ptr(walk),
+                                             _ptr(accept_pos), _ptr(accept_psnr), cap, int(K), int(batches),
+                                             _stream(stream)), "hbx_dbs_walk_psf")
+
     def commit_flip(self, base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats,
                     k_dev: torch.Tensor, stream=None):
         _lib.check(self.lib.hbx_commit_flip(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),

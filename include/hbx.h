@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 4
+#define HBX_ABI_VERSION 5
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -231,6 +231,47 @@ int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_
                         double* prev_psnr, float* field, float* intensity, const int64_t* flips,
                         const double* psnr_out, const double* group_stats, const int32_t* k,
                         void* stream);
+
+/* Device-resident greedy DBS walk (ABI v5): the whole loop of DBS.py:247-294 /
+ * DBS_1024_24.py:313-422 -- visit order[pos..], keep a flip iff PSNR strictly
+ * improves -- as speculative batches that never return to the host.  Each
+ * batch evaluates the next K candidates on the incremental-field path (as
+ * hbx_eval_flips_psf); a one-block launch picks the first improving one in
+ * visiting order, toggles its mask bit, updates base_chan_stats and the walk
+ * state and appends (position, psnr) to the accept log; a third launch
+ * rewrites the accepted plane's field and group intensity.  `batches` batches
+ * are enqueued per call with no host synchronisation; batches after the walk
+ * is done (or halted) cost three empty launches.  The accept sequence is the
+ * serial loop's: every candidate before an accepted one was evaluated against
+ * exactly the state the serial loop would have had.
+ *
+ * The walk state lives in DEVICE memory (caller-owned; commit_ch = -1 and the
+ * counters zero at the start); the caller reads it back between calls.  When halt == 1
+ * (after every refresh_every-th accept) the caller re-propagates field,
+ * intensity and base_chan_stats exactly (hbx_simulate / hbx_propagate), sets
+ * prev_psnr to the exact PSNR and clears halt. */
+typedef struct hbx_dbs_walk {
+  int64_t pos;             /* next position of `order` to visit                  */
+  int64_t total;           /* positions to visit (order length or a prefix)      */
+  int64_t accepted;        /* accepts so far (log entries written: min(., cap))  */
+  int64_t batches;         /* speculative batches evaluated                      */
+  double prev_psnr;        /* PSNR of the current base                           */
+  double init_psnr;        /* PSNR at the start of the walk                      */
+  double last_psnr;        /* PSNR of the last visited candidate                 */
+  double stop_diff;        /* DBS_ratio_0.5.py:366-372 early stop threshold      */
+  int32_t stop_enabled;    /* 1: done once prev_psnr - init_psnr >= stop_diff    */
+  int32_t refresh_every;   /* halt after every refresh_every-th accept (0: never) */
+  int32_t done;            /* 1: pos == total, or stopped early                  */
+  int32_t halt;            /* 1: paused for an exact refresh (caller clears)     */
+  int32_t stopped_early;
+  int32_t commit_ch;       /* internal: pending commit channel, -1 = none        */
+  int32_t commit_pix;      /* internal                                           */
+  int32_t reserved[3];     /* zero                                               */
+} hbx_dbs_walk_t;
+int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
+                     double* base_chan_stats, float* field, float* intensity, const int64_t* order,
+                     hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                     int64_t accept_cap, int32_t K, int32_t batches, void* stream);
 
 /* Incremental-field ("PSF") mode (reported separately from
  * the FFT-mode headline).  tt.simulate is linear, so flipping pixel (c, r, col)

@@ -59,7 +59,7 @@ int main(void) {{ printf("%zu\\n", sizeof({struct_name})); return 0; }}
 
 
 @pytest.mark.parametrize("cname,pyname", [("hbx_optics_t", "Optics"), ("hbx_env_buffers_t", "EnvBuffers"),
-                                          ("hbx_env_params_t", "EnvParams")])
+                                          ("hbx_env_params_t", "EnvParams"), ("hbx_dbs_walk_t", "DbsWalk")])
 def test_struct_layout_matches(cname, pyname):
     from hbx import _lib
     assert C.sizeof(getattr(_lib, pyname)) == _c_sizeof(cname)

@@ -588,9 +588,11 @@ def test_premodel_on_gpu_feeds_env_reset():
     vec.close()
 
 
+@pytest.mark.parametrize("mode", ["psf", "psf_host"])
 @pytest.mark.parametrize("refresh", [0, 64])
-def test_dbs_greedy_incremental_mode(golden_dir, refresh):
-    """Greedy DBS with candidates on the incremental-field path
+def test_dbs_greedy_incremental_mode(golden_dir, refresh, mode):
+    """Greedy DBS with candidates on the incremental-field path -- the
+    device-resident walk (hbx_dbs_walk_psf) and the host-decided batches
     (hbx_eval_flips_psf / hbx_commit_flip_psf): the serial accept sequence of
     the 4096-flip oracle trace, with and without periodic exact refresh."""
     import hbx
@@ -598,13 +600,60 @@ def test_dbs_greedy_incremental_mode(golden_dir, refresh):
     d = load(golden_dir, "dbs_trace_64.npz")
     plan = hbx.Plan(dev_cfg(small_rgb()), max_jobs=128)
     mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
-    res = dbs.greedy(plan, mask, torch.from_numpy(d["target"]).cuda(), d["order"], mode="psf",
+    res = dbs.greedy(plan, mask, torch.from_numpy(d["target"]).cuda(), d["order"], mode=mode,
                      refresh_every=refresh)
     want_pos = np.nonzero(d["accepted"])[0]
     got = np.array(res.accepted_positions)
     assert len(got) == len(want_pos) and np.array_equal(got, want_pos)
     assert abs(res.final_psnr - float(d["final_psnr"])) <= PSNR_TOL
     assert np.array_equal(mask.cpu().numpy().view("<u8"), d["final_mask_bits"])
+
+
+def test_dbs_walk_early_stop_and_prefix():
+    """Device walk: DBS_ratio_0.5.py's early stop (stop_diff) against the serial
+    oracle, and a max_candidates prefix ends exactly at the prefix."""
+    import hbx
+    from hbx import dbs
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 21)
+    order = np.random.default_rng(3).permutation(ocfg.channels * 64 * 64)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=8)
+    env = O.OracleEnv(ocfg, accept_rule=1)
+    env.reset(pre, tgt)
+    acc, ps, final = O.dbs_greedy(env, order, stop_diff=0.05)
+    mask = hbx.pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+    res = dbs.greedy(plan, mask, torch.from_numpy(tgt).cuda(), order, stop_diff=0.05, mode="psf")
+    assert res.stopped_early
+    assert res.steps == len(acc)
+    assert abs(res.final_psnr - final) <= PSNR_TOL
+    mask = hbx.pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+    res = dbs.greedy(plan, mask, torch.from_numpy(tgt).cuda(), order, mode="psf", max_candidates=777)
+    assert res.steps == 777 and not res.stopped_early
+    assert all(p < 777 for p in res.accepted_positions)
+
+
+@pytest.mark.parametrize("field_kind", [0, 1])
+def test_dbs_walk_matches_host_batches_1024(field_kind):
+    """1024 x 24 RGB: the device-resident walk and the host-decided psf batches
+    accept the same positions over a 3000-candidate prefix and end on the same
+    mask; the final PSNR agrees with an exact re-propagation."""
+    import hbx
+    from hbx import dbs
+    cfg = hbx.rgb_config(1024, field_kind=field_kind)
+    g = torch.Generator(device="cuda").manual_seed(31)
+    pre = torch.rand((24, 1024, 1024), generator=g, device="cuda")
+    tgt = torch.rand((3, 1024, 1024), generator=g, device="cuda")
+    order = np.random.default_rng(3).permutation(24 * 1024 * 1024)[:3000]
+    plan = hbx.Plan(cfg, max_jobs=64)
+    m1 = hbx.pack_bits(pre >= 0.5)
+    m2 = m1.clone()
+    r1 = dbs.greedy(plan, m1, tgt, order, mode="psf")
+    r2 = dbs.greedy(plan, m2, tgt, order, mode="psf_host")
+    assert r1.steps == r2.steps == 3000
+    assert r1.accepted_positions == r2.accepted_positions
+    assert torch.equal(m1, m2)
+    _, _, ps = plan.propagate(m1[None], tgt[None], want_intensity=False)
+    assert abs(float(ps[0]) - r1.final_psnr) <= PSNR_TOL
 
 
 # ---------------------------------------------------------------------------

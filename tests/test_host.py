@@ -200,3 +200,14 @@ def test_crop_config():
     import hbx
     c = hbx.crop_config(hbx.rgb_config(1024), 64)
     assert (c.height, c.width, c.groups, c.planes) == (896, 896, 3, 8)
+
+
+def test_walk_k_choice():
+    """Device-walk speculation depth: short batches at high acceptance and
+    large sides, long ones when acceptance is rare or candidates are cheap."""
+    from hbx.dbs import walk_k
+    assert walk_k(0.5, 1024) <= 4
+    assert walk_k(0.01, 1024) > walk_k(0.5, 1024)
+    assert walk_k(0.5, 64) > walk_k(0.5, 1024)
+    assert walk_k(1e-9, 1024, 1, 256) == 256
+    assert 1 <= walk_k(1.0, 1024) <= 2

@@ -1,0 +1,32 @@
+"""Greedy-DBS prefix on the device walk at 1024 x 24 (for rocprofv3 kernel traces):
+python tools/walk_prof.py [n_flips] [mode]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "binary-hologram-reinforcement-learning_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hbx  # noqa: E402
+from hbx import dbs  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+mode = sys.argv[2] if len(sys.argv) > 2 else "psf"
+cfg = hbx.rgb_config(1024)
+g = torch.Generator(device="cuda").manual_seed(0)
+pre = torch.rand((24, 1024, 1024), generator=g, device="cuda")
+tgt = torch.rand((3, 1024, 1024), generator=g, device="cuda")
+order = np.random.default_rng(3).permutation(24 * 1024 * 1024)[:n]
+plan = hbx.Plan(cfg, max_jobs=256)
+m = hbx.pack_bits(pre >= 0.5)
+dbs.greedy(plan, m.clone(), tgt, order[:256], mode=mode)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+r = dbs.greedy(plan, m, tgt, order, mode=mode)
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+print(f"{mode}: {r.steps} candidates, {len(r.accepted_positions)} accepted, {r.launches} batches, "
+      f"{dt:.3f} s, {r.steps / dt:.1f} candidates/s, {1e6 * dt / r.launches:.1f} us/batch")
