@@ -140,6 +140,10 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       const double a = -2.0 * M_PI * (double)((t * k1) % N) / (double)N;
       tw[(size_t)k1 * R + t] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
+  if (R == 0) {   // N = 896: fused three-pass path unless HBX_GENERIC896=1 (the composed path)
+    const char* ev = std::getenv("HBX_GENERIC896");
+    pd.fused896 = (ev && ev[0] && ev[0] != '0') ? 0 : 1;
+  }
   if (R == 0)   // N = 896: [k1 < 28][t < 32] = W896^{t k1}
     for (int k1 = 0; k1 < 28; ++k1)
       for (int t = 0; t < 32; ++t) {
@@ -266,7 +270,7 @@ size_t hbx_plan_workspace_bytes(hbx_plan_t p) { return p ? p->ws_bytes : 0; }
 int hbx_plan_pipeline(hbx_plan_t p) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (p->pd.R == 0) return HBX_PIPE_GENERIC;
+  if (p->pd.R == 0) return p->pd.fused896 ? HBX_PIPE_THREE_PASS : HBX_PIPE_GENERIC;
   return (p->pd.R == 32 && p->pd.colbits) ? HBX_PIPE_COLBITS : HBX_PIPE_THREE_PASS;
 }
 

@@ -120,6 +120,7 @@ struct PlanDev {
   int32_t* psf_order;  // [max_jobs] jobs sorted by colour group (launch order)
   float* zero_row;     // [N] zeros: the target row of a propagation without a target
   int colbits;         // N = 1024: bits -> column pass without the A intermediate (hbx_colbits.hip)
+  int fused896;        // N = 896: fused three-pass path (hbx_passes896.hip); 0 = composed (hbx_generic.hip)
   PassTimer* timer;    // nullable
 };
 
@@ -165,6 +166,9 @@ hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const ui
                     const float* target, float* inten_out, float2* field_out, hipStream_t st);
 // generic propagation (N = 896, hbx_generic.hip): prep -> 2-D FFT -> H -> inverse
 // 2-D FFT -> |U|^2 mean + partial sums, on the transposing row-FFT kernel
+// fused three-pass propagation at N = 896 (hbx_passes896.hip)
+hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
+                        const float* target, float* inten_out, float2* field_out, hipStream_t st);
 hipError_t run_jobs_generic(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                             const float* target, float* inten_out, float2* field_out, hipStream_t st);
 // 2-D FFT of n_planes [N][N] complex planes in a (result in a; b is scratch of

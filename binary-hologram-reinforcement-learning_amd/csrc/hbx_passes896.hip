@@ -1,0 +1,406 @@
+// hbx_passes896.hip -- the fused three-pass propagation at N = 896, the
+// 64-pixel centre crop of a 1024 mask that env_1024_24_128.py:144-149 and
+// DBS_1024_24-128.py:210-216 propagate.
+//
+// Same structure as the N = R^2 passes (hbx_passes.hip), on the 28 x 32
+// lane-group FFT of hbx_fft.hpp (natural layout: lane t < 32, register j < 28
+// holds x[t + 32 j]; slot layout: lane k1 < 28, register k2 < 32 holds
+// X[k1 + 28 k2]):
+//
+//   k_rowfwd896  8 rows of a plane pair per block: bits -> one complex FFT
+//                per row pair (plane a real, plane b imaginary) -> Hermitian
+//                split -> half spectrum kx < 448 (Nyquist in Im of kx = 0) ->
+//                LDS tile transpose -> A[kx][y0..y0+8)   [read N^2/8, write 4 N^2 B per plane]
+//   k_col896     one lane group per half-spectrum line kx: FFT over y ->
+//                x H and x conj H (H even in fx and ky) -> two IFFTs -> B lines
+//                kx and N - kx (448 for kx = 0)           [read 4 N^2, write 8 N^2]
+//   k_rowinv896  8 rows per block, all P planes: LDS tile transpose of the B
+//                rows (next plane prefetched) -> IFFT over kx -> |U|^2 -> plane
+//                mean -> f64 partials of (I T, I^2, T^2)  [read 8 N^2 per plane + 4 N^2]
+//
+// A is [kx < 448][y], B is [kx < 896][y] (column-major lines).  It replaces
+// the composed path of hbx_generic.hip (kept behind HBX_GENERIC896=1), which
+// moved ~10 plane-sized round trips per job instead of 3.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbx_fft.hpp"
+#include "hbx_internal.hpp"
+#include "hbx_rowcol.hpp"
+
+namespace hbx {
+
+namespace {
+
+constexpr int kN = 896;
+constexpr int kR = 32;                         // lanes per group
+constexpr int kL = 28;                         // slot lanes / natural registers
+constexpr int kGPB = 8;                        // rows (lines) per 256-thread block
+constexpr int kRB = kN / kGPB;                 // 112 row blocks
+constexpr int kHalf = kN / 2;                  // 448 half-spectrum lines
+constexpr size_t kPlaneA = (size_t)kHalf * kN;
+constexpr size_t kPlaneB = (size_t)kN * kN;
+constexpr int kSCR = kGPB * kR * (kR + 1);     // padded transpose scratch
+constexpr int kWPR = kN / 32;                  // 32-bit mask words per row (28)
+static_assert(kN * kGPB <= kSCR, "the row tile must fit in the scratch area");
+
+// conj Z[N - k] for the slot-layout element k = k1 + 28 k2 (lane k1 < 28,
+// register k2): lane 28 - k1, register 31 - k2; lane 0 keeps its own
+// register (32 - k2) mod 32.  Lanes 28..31 get don't-care values.
+__device__ __forceinline__ float2 mirror_conj896(const float2 (&v)[32], int k2, int t, int lane_base) {
+  const int src = lane_base + ((t > 0 && t < kL) ? kL - t : 0);
+  float2 p;
+  p.x = __shfl(v[31 - k2].x, src, 64);
+  p.y = __shfl(v[31 - k2].y, src, 64);
+  const float2 own = v[(32 - k2) & 31];
+  return conjf2(t == 0 ? own : p);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Pass 1
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_rowfwd896(const JobDesc* __restrict__ jobs,
+                                                      const uint32_t* __restrict__ mask,
+                                                      float2* __restrict__ ws_a,
+                                                      const float2* __restrict__ tw_glob, int P, int CH,
+                                                      float va, float vb) {
+  __shared__ float2 tw[kN];
+  __shared__ __attribute__((aligned(16))) float2 lds[kSCR];
+  for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / kR;
+  const int t = threadIdx.x % kR;
+  const int lane_base = (threadIdx.x & 63) - t;
+  int bid = xcd_pair<kRB>(blockIdx.x);
+  const int rb = bid % kRB;
+  bid /= kRB;
+  const int q = bid % (P / 2);
+  const int j = bid / (P / 2);
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;  // uniform per block
+  const int y0 = rb * kGPB;
+  const int y = y0 + grp;
+  const int pa = 2 * q, pb = 2 * q + 1;
+
+  const uint32_t* rowa = mask + ((size_t)jb.env * CH + jb.group * P + pa) * kN * kWPR + (size_t)y * kWPR;
+  const uint32_t* rowb = rowa + (size_t)kN * kWPR;
+  uint32_t wa[kWPR], wb[kWPR];
+#pragma unroll
+  for (int i = 0; i < kWPR / 4; ++i) {
+    const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
+    const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
+    wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
+    wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
+  }
+  if (jb.flip_plane >= 0 && jb.flip_pix / kN == y) {  // env.py:164 flip, on the fly
+    const int col = jb.flip_pix % kN;
+    const uint32_t bit = 1u << (col & 31);
+#pragma unroll
+    for (int i = 0; i < kWPR; ++i) {
+      if (i == (col >> 5)) {
+        if (jb.flip_plane == pa) wa[i] ^= bit;
+        if (jb.flip_plane == pb) wb[i] ^= bit;
+      }
+    }
+  }
+  float2 v[32];
+#pragma unroll
+  for (int jj = 0; jj < kL; ++jj)   // x = t + 32 jj is bit t of word jj
+    v[jj] = make_float2(fmaf(vb, (float)((wa[jj] >> t) & 1u), va), fmaf(vb, (float)((wb[jj] >> t) & 1u), va));
+#pragma unroll
+  for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
+  __syncthreads();  // tw visible
+  fft896_ns<false>(v, t, PaddedScratch<kR>{lds + grp * kR * (kR + 1)}, tw);
+  lds_barrier();    // every group is done with its scratch: reuse as the tile
+
+  // Hermitian split of the slot-layout spectrum (kx = t + 28 k2 < 448: k2 < 16)
+  float2* tile = lds;
+  const float2 zny = v[16];  // Z[448] on lane 0
+#pragma unroll
+  for (int k2 = 0; k2 < 16; ++k2) {
+    const float2 z = v[k2];
+    const float2 m = mirror_conj896(v, k2, t, lane_base);
+    float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
+    float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+    if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
+      fa = make_float2(z.x, zny.x);
+      fb = make_float2(z.y, zny.y);
+    }
+    if (t < kL) {
+      const int kx = t + kL * k2;
+      tile[tile_pos<kR, kGPB>(kx, grp)] = fa;
+      tile[tile_pos<kR, kGPB>(kHalf + kx, grp)] = fb;
+    }
+  }
+  lds_barrier();
+  // A[pa|pb][kx][y0 .. y0+8): 16 B per thread per chunk
+  float2* base = ws_a + ((size_t)j * P + pa) * kPlaneA;
+  constexpr int CHUNKS = kN * kGPB / 2;
+  static_assert(CHUNKS % 256 == 0, "chunking");
+#pragma unroll
+  for (int i = 0; i < CHUNKS / 256; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int r2 = (c % (kGPB / 2)) * 2;
+    const int line = c / (kGPB / 2);   // pl * 448 + kx
+    const float2 a = tile[tile_pos<kR, kGPB>(line, r2)];
+    const float2 b = tile[tile_pos<kR, kGPB>(line, r2 + 1)];
+    const int pl = line / kHalf;
+    *reinterpret_cast<float4*>(base + (size_t)pl * kPlaneA + (size_t)(line - pl * kHalf) * kN + y0 + r2) =
+        make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2: one lane group per input line and both of its output lines (as
+// k_col2): FFT over y -> Z (slot layout); W = Z conj H to the group's scratch
+// (+ a pad copy of W[0]) while v becomes Z H; M H = conj W(N - ky) read back
+// (H is even in ky); IFFT of Z H -> B line kx, of M H -> B line N - kx
+// (kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448)
+// ---------------------------------------------------------------------------
+constexpr int kColIter = 4;
+constexpr int kColLB = kHalf / (kGPB * kColIter);   // 14 blocks per plane
+static_assert(kHalf % (kGPB * kColIter) == 0, "line blocking");
+
+__global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ jobs,
+                                                   const float2* __restrict__ ws_a,
+                                                   float2* __restrict__ ws_b,
+                                                   const float2* __restrict__ htab,
+                                                   const float2* __restrict__ tw_glob, int P) {
+  __shared__ float2 tw[kN];
+  __shared__ float2 scratch[kSCR];
+  for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / kR;
+  const int t = threadIdx.x % kR;
+  int bid = blockIdx.x;
+  const int lb = bid % kColLB;
+  bid /= kColLB;
+  const int p = bid % P;
+  const int j = bid / P;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;
+  const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * kPlaneA, (unsigned)(kPlaneA * 8));
+  const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * kPlaneB, (unsigned)(kPlaneB * 8));
+  const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (kHalf + 1) * kN,
+                                               (unsigned)((kHalf + 1) * kN * 8));
+  const PaddedScratch<kR> sc{scratch + grp * kR * (kR + 1)};
+  const int k1 = t < kL ? t : 0;   // slot lane (28..31 carry don't-care values)
+  const float2* mrow = (t > 0 && t < kL) ? sc.at(kL - t, 31) : sc.at(0, 32);
+  constexpr int KSTEP = kColLB * kGPB;
+  const int kx0 = lb * kGPB + grp;
+
+  float2 v[32];
+  {
+    const int vo = (kx0 * kN + t) * 8;
+#pragma unroll
+    for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2(ra, vo, jj * kR * 8);
+#pragma unroll
+    for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
+  }
+  lds_barrier();  // tw visible (the line loads stay in flight)
+
+#pragma unroll 1
+  for (int it = 0; it < kColIter; ++it) {
+    const int kx = kx0 + it * KSTEP;
+    const bool dc = (kx == 0);
+    const int vh = (kx * kN + k1) * 8;   // H(kx, ky = k1 + 28 k2) at vh + k2 * 28 * 8
+    fft896_ns<false>(v, t, sc, tw);
+    wave_sync();
+    if (!dc) {
+#pragma unroll
+      for (int c8 = 0; c8 < 32; c8 += 8) {
+        float2 hb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * kL * 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k2 = c8 + i;
+          const float2 w = cmulc(v[k2], hb[i]);
+          *sc.at(t, k2) = w;
+          if (k2 == 0) *sc.at(t, 32) = w;
+          v[k2] = cmul(v[k2], hb[i]);
+        }
+      }
+    } else {  // kx = 0: plain Z through the scratch
+#pragma unroll
+      for (int k2 = 0; k2 < 32; ++k2) *sc.at(t, k2) = v[k2];
+      *sc.at(t, 32) = v[0];
+    }
+    wave_sync();
+    float2 m[32];
+#pragma unroll
+    for (int k2 = 0; k2 < 32; ++k2) m[k2] = conjf2(mrow[-k2]);
+    if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448
+      const int vn = (kHalf * kN + k1) * 8;
+#pragma unroll
+      for (int k2 = 0; k2 < 32; ++k2) {
+        const float2 z = v[k2], mm = m[k2];
+        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), buf_ld2(rh, vh, k2 * kL * 8));
+        m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * kL * 8));
+      }
+    }
+    fft896_sn<true>(v, t, sc, tw);
+    {
+      const int vo = (kx * kN + t) * 8;
+#pragma unroll
+      for (int jj = 0; jj < kL; ++jj) buf_st2(v[jj], rb, vo, jj * kR * 8);
+    }
+    if (it + 1 < kColIter) {  // next line in flight under the second inverse FFT
+      const int vo = ((kx + KSTEP) * kN + t) * 8;
+#pragma unroll
+      for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2(ra, vo, jj * kR * 8);
+#pragma unroll
+      for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
+    }
+    fft896_sn<true>(m, t, sc, tw);
+    {
+      const int vo = ((dc ? kHalf : kN - kx) * kN + t) * 8;
+#pragma unroll
+      for (int jj = 0; jj < kL; ++jj) buf_st2(m[jj], rb, vo, jj * kR * 8);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 3
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict__ jobs,
+                                                      const float2* __restrict__ ws_b,
+                                                      const float* __restrict__ target,
+                                                      const float2* __restrict__ tw_glob, int P, int G,
+                                                      double* __restrict__ partial,
+                                                      float* __restrict__ inten_out,
+                                                      float2* __restrict__ field_out, size_t tmask) {
+  constexpr int CH16 = kN * kGPB / 2;   // 16-B chunks per plane tile
+  constexpr int PER = CH16 / 256;
+  static_assert(CH16 % 256 == 0, "chunking");
+  __shared__ float2 tw[kN];
+  __shared__ __attribute__((aligned(16))) float2 tile[kSCR];
+  __shared__ double red[kGPB][3];
+  for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / kR;
+  const int t = threadIdx.x % kR;
+  const int bid = xcd_pair<kRB>(blockIdx.x);
+  const int rb = bid % kRB;
+  const int j = bid / kRB;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) {
+    if (threadIdx.x == 0) {
+      double* o = partial + ((size_t)j * kRB + rb) * 3;
+      o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
+    }
+    return;
+  }
+  const int y0 = rb * kGPB;
+  const int y = y0 + grp;
+  const float2* jbase = ws_b + (size_t)j * P * kPlaneB;
+  const int k1 = t < kL ? t : 0;
+
+  float4 pre[PER];   // this thread's share of a plane tile, one plane ahead
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
+    pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * kN + y0 + r2);
+  }
+  float acc[kL];
+#pragma unroll
+  for (int k = 0; k < kL; ++k) acc[k] = 0.0f;
+
+#pragma unroll 1
+  for (int p = 0; p < P; ++p) {
+    lds_barrier();  // previous plane's scratch use is over (also publishes tw)
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
+      tile[tile_pos<kR, kGPB>(line, r2)] = make_float2(pre[i].x, pre[i].y);
+      tile[tile_pos<kR, kGPB>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
+    }
+    if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
+      const float2* nb = jbase + (size_t)(p + 1) * kPlaneB;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
+        pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * kN + y0 + r2);
+      }
+    }
+    lds_barrier();
+    float2 v[32];   // slot layout: lane k1, register k2 -> kx = k1 + 28 k2
+#pragma unroll
+    for (int k2 = 0; k2 < 32; ++k2) v[k2] = tile[tile_pos<kR, kGPB>(k1 + kL * k2, grp)];
+    lds_barrier();  // tile consumed: reuse it as transpose scratch
+    fft896_sn<true>(v, t, PaddedScratch<kR>{tile + grp * kR * (kR + 1)}, tw);
+#pragma unroll
+    for (int k = 0; k < kL; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+    if (field_out) {  // exact field of this plane (incremental mode init / refresh)
+      float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * kN + y) * kN;
+#pragma unroll
+      for (int k = 0; k < kL; ++k) frow[t + kR * k] = v[k];
+    }
+  }
+
+  const float invp = 1.0f / (float)P;
+  const float* trow = target + ((((size_t)jb.env * G + jb.group) * kN + y) * kN & tmask);
+  double sxy = 0.0, sxx = 0.0, syy = 0.0;
+#pragma unroll
+  for (int k = 0; k < kL; ++k) {
+    const float I = acc[k] * invp;
+    const float T = trow[t + kR * k];
+    sxy = fma((double)I, (double)T, sxy);
+    sxx = fma((double)I, (double)I, sxx);
+    syy = fma((double)T, (double)T, syy);
+    acc[k] = I;
+  }
+  if (inten_out) {
+    float* orow = inten_out + ((size_t)j * kN + y) * kN;
+#pragma unroll
+    for (int k = 0; k < kL; ++k) orow[t + kR * k] = acc[k];
+  }
+#pragma unroll
+  for (int off = kR / 2; off >= 1; off >>= 1) {
+    sxy += __shfl_xor(sxy, off, 64);
+    sxx += __shfl_xor(sxx, off, 64);
+    syy += __shfl_xor(syy, off, 64);
+  }
+  if (t == 0) { red[grp][0] = sxy; red[grp][1] = sxx; red[grp][2] = syy; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, cc = 0.0;
+    for (int g = 0; g < kGPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
+    double* o = partial + ((size_t)j * kRB + rb) * 3;
+    o[0] = a; o[1] = b; o[2] = cc;
+  }
+}
+
+__global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,
+                                  double* __restrict__ job_stats);
+
+hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
+                        const float* target, float* inten_out, float2* field_out, hipStream_t st) {
+  const int P = pd.P;
+  const int CH = pd.G * pd.P;
+  PassTimer* tm = pd.timer;
+  if (tm) tm->begin(0, st);
+  hipLaunchKernelGGL(k_rowfwd896, dim3((unsigned)n_jobs * (P / 2) * kRB), dim3(256), 0, st, jobs, mask, pd.ws_a,
+                     pd.tw, P, CH, pd.va, pd.vb);
+  if (tm) tm->end(0, n_jobs, st);
+  if (tm) tm->begin(1, st);
+  hipLaunchKernelGGL(k_col896, dim3((unsigned)n_jobs * P * kColLB), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
+                     pd.htab, pd.tw, P);
+  if (tm) tm->end(1, n_jobs, st);
+  if (tm) tm->begin(2, st);
+  hipLaunchKernelGGL(k_rowinv896, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
+                     target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                     target ? ~(size_t)0 : (size_t)0);
+  if (tm) tm->end(2, n_jobs, st);
+  hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial, n_jobs, kRB,
+                     pd.job_stats);
+  return hipGetLastError();
+}
+
+}  // namespace hbx

@@ -1,0 +1,69 @@
+// hbx_rowcol.hpp -- helpers shared by the row / column passes (hbx_passes.hip,
+// hbx_passes896.hip): LDS tile swizzle, XCD-aware row-block order, buffer
+// descriptors of wave-uniform planes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hbx_fft.hpp"
+
+namespace hbx {
+
+// Position of element (line, r) in an LDS tile [line][GPB rows], r XOR-swizzled
+// by a function of (line mod R) only: lane t of a group reading line t + R*j
+// then addresses base_t + j*R*GPB (immediate offsets, no per-j address VGPRs),
+// ds_read_b64 is conflict-free and ds_write_b64 at most 2-way (checked
+// exhaustively for R = 8, 16, 32).
+template <int R, int GPB = 256 / R>
+__device__ __forceinline__ int tile_pos(int line, int r) {
+  if constexpr (GPB == 16) {
+    // 16 rows (512-thread blocks, N = 1024): swizzle (line mod 16) ^ bit 4 of
+    // line -- conflict-free for the lane-row reads / writes and the 16-B chunk
+    // writes; the chunk reads of k_rowfwd stay 2-way (checked exhaustively)
+    return line * GPB + (r ^ (((line & 15) ^ ((line >> 4) & 1)) & (GPB - 1)));
+  } else {
+    constexpr int SR = ilog2c(32 / GPB);
+    constexpr int SL = ilog2c(GPB / 8);
+    return line * GPB + (r ^ ((((line & (R - 1)) >> SR) << SL) & (GPB - 1)));
+  }
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// buffer descriptor of a wave-uniform plane (cdna_hip_programming.md T8 recipe)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float2 buf_ld2(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+}
+
+__device__ __forceinline__ void buf_st2(float2 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
+}
+
+// Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
+// the 8 XCDs; placement is a speed hint only, never relied on for
+// correctness).  The row passes touch 64-B pieces of every 8-KB line, the
+// piece for rows y0..y0+7: keep GS consecutive row blocks on one XCD so each
+// line is read / written as GS*64 contiguous bytes through one L2.  Measured
+// on 1024x24, 128 envs (k_rowfwd / k_rowinv ms): no remap 1.34 / 2.75,
+// GS=2 1.18 / 2.43, GS=4 1.17 / 2.40, GS=8 1.12 / 2.08, GS=16 1.12 / 1.98.
+#ifndef HBX_XCD_GROUP
+#define HBX_XCD_GROUP 16
+#endif
+template <int RB>
+__device__ __forceinline__ int xcd_pair(int bid) {
+  constexpr int GS = (RB / 8 < HBX_XCD_GROUP) ? RB / 8 : HBX_XCD_GROUP;
+  constexpr int SPAN = 8 * (GS > 0 ? GS : 1);
+  if constexpr (GS > 1 && RB % SPAN == 0)
+    return (bid / SPAN) * SPAN + (bid % 8) * GS + (bid / 8) % GS;
+  else return bid;
+}
+
+}  // namespace hbx

@@ -671,6 +671,55 @@ def _crop_inputs(seed):
     return ocfg, pre_c, tgt_c, bits
 
 
+def _plan_896(cfg, max_jobs, generic):
+    """Plan on the fused 896 path (default) or the composed one (HBX_GENERIC896=1)."""
+    import hbx
+    old = os.environ.pop("HBX_GENERIC896", None)
+    try:
+        if generic:
+            os.environ["HBX_GENERIC896"] = "1"
+        plan = hbx.Plan(cfg, max_jobs=max_jobs)
+        assert plan.pipeline == (hbx._lib.PIPE_GENERIC if generic else hbx._lib.PIPE_THREE_PASS)
+        return plan
+    finally:
+        os.environ.pop("HBX_GENERIC896", None)
+        if old is not None:
+            os.environ["HBX_GENERIC896"] = old
+
+
+@pytest.mark.parametrize("field_kind", [0, 1])
+def test_crop_896_fused_matches_composed(field_kind):
+    """N = 896: the fused three-pass path (hbx_passes896.hip) against the composed
+    mixed-radix path on 6 envs (18 jobs), flips at the row / column edges of
+    every slot lane class: stats rtol 2e-6, intensity and field 2e-6 * max."""
+    import hbx
+    cfg = hbx.rgb_config(896, field_kind=field_kind)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    pre = torch.rand((6, 24, 896, 896), generator=g, device="cuda")
+    bits = hbx.pack_bits(pre >= 0.5)
+    tgt = torch.rand((6, 3, 896, 896), generator=g, device="cuda")
+    new = _plan_896(cfg, 18, generic=False)
+    old = _plan_896(cfg, 18, generic=True)
+    a = new.propagate(bits, tgt)
+    b = old.propagate(bits, tgt)
+    torch.cuda.synchronize()
+    assert torch.allclose(a[1], b[1], rtol=2e-6, atol=0)
+    assert float((a[0] - b[0]).abs().max()) <= 2e-6 * float(b[0].abs().max())
+    assert float((a[2] - b[2]).abs().max()) <= 1e-5
+    fa, _ = new.simulate(bits[:1])
+    fb, _ = old.simulate(bits[:1])
+    assert float((fa - fb).abs().max()) <= 2e-6 * float(fb.abs().max())
+    n = 896 * 896
+    fl = [c * n + r * 896 + x for c in (0, 7, 8, 16, 23) for (r, x) in
+          ((0, 0), (895, 895), (447, 27), (448, 28), (5, 447), (300, 448), (1, 895 - 31))]
+    flips = torch.tensor(fl, dtype=torch.int64, device="cuda")
+    st0 = a[1][0].contiguous()
+    pa, _ = new.eval_flips(bits[0], tgt[0], st0, flips)
+    pb, _ = old.eval_flips(bits[0], tgt[0], st0, flips)
+    torch.cuda.synchronize()
+    assert float((pa - pb).abs().max()) <= 2e-5
+
+
 def test_crop_896_propagate_vs_oracle():
     import hbx
     ocfg, pre, tgt, bits = _crop_inputs(7)
