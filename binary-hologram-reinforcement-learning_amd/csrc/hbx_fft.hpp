@@ -549,7 +549,9 @@ __device__ __forceinline__ void dft28(float2 (&v)[32]) {
 
 // 896-point FFT by 32 lanes, natural layout in -> slot layout out.
 // tw896: LDS [k1 < 28][t < 32] = W896^{t k1} (forward sign); INV conjugates.
-template <bool INV, class Scratch>
+// SCALAR: scalar-f32 32-point DFTs (fewer live registers than the packed ones
+// when a kernel keeps two lines in flight)
+template <bool INV, bool SCALAR = false, class Scratch>
 __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
   asm volatile("" ::: "memory");
   dft28<INV>(v);
@@ -567,15 +569,17 @@ __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch&
 #pragma unroll
   for (int tt = 0; tt < 32; ++tt) v[tt] = *sc.at(tt, k1);
   wave_sync();
-  dft_reg<32, INV>(v);
+  if constexpr (SCALAR) dft_reg_scalar<32, INV>(v);
+  else dft_reg<32, INV>(v);
 }
 
 // 896-point FFT by 32 lanes, slot layout in -> natural layout out (adjoint of
 // fft896_ns: the same stages in reverse order with the opposite sign)
-template <bool INV, class Scratch>
+template <bool INV, bool SCALAR = false, class Scratch>
 __device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
   asm volatile("" ::: "memory");
-  dft_reg<32, INV>(v);        // over k2 -> index t (the natural lane)
+  if constexpr (SCALAR) dft_reg_scalar<32, INV>(v);   // over k2 -> index t (the natural lane)
+  else dft_reg<32, INV>(v);
   wave_sync();
   // lane k1 (< 28) holds B[k1][t] for t = 0..31 in v[t]
   if (t < 28) {

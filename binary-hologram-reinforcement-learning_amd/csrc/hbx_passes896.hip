@@ -159,6 +159,16 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd896(const JobDesc* __restrict_
 // (H is even in ky); IFFT of Z H -> B line kx, of M H -> B line N - kx
 // (kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448)
 // ---------------------------------------------------------------------------
+#ifndef HBX_896_COL_PACKED
+constexpr bool kColScalar = true;    // packed 32-point DFTs spill with two lines live
+#else
+constexpr bool kColScalar = false;
+#endif
+#ifdef HBX_896_INV_SCALAR
+constexpr bool kInvScalar = true;
+#else
+constexpr bool kInvScalar = false;
+#endif
 constexpr int kColIter = 4;
 constexpr int kColLB = kHalf / (kGPB * kColIter);   // 14 blocks per plane
 static_assert(kHalf % (kGPB * kColIter) == 0, "line blocking");
@@ -206,7 +216,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * kN + k1) * 8;   // H(kx, ky = k1 + 28 k2) at vh + k2 * 28 * 8
-    fft896_ns<false>(v, t, sc, tw);
+    fft896_ns<false, kColScalar>(v, t, sc, tw);
     wave_sync();
     if (!dc) {
 #pragma unroll
@@ -241,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
         m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * kL * 8));
       }
     }
-    fft896_sn<true>(v, t, sc, tw);
+    fft896_sn<true, kColScalar>(v, t, sc, tw);
     {
       const int vo = (kx * kN + t) * 8;
 #pragma unroll
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
 #pragma unroll
       for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
     }
-    fft896_sn<true>(m, t, sc, tw);
+    fft896_sn<true, kColScalar>(m, t, sc, tw);
     {
       const int vo = ((dc ? kHalf : kN - kx) * kN + t) * 8;
 #pragma unroll
@@ -276,6 +286,10 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
   constexpr int CH16 = kN * kGPB / 2;   // 16-B chunks per plane tile
   constexpr int PER = CH16 / 256;
   static_assert(CH16 % 256 == 0, "chunking");
+#ifndef HBX_896_INV_PF
+#define HBX_896_INV_PF 8
+#endif
+  constexpr int PF = HBX_896_INV_PF < PER ? HBX_896_INV_PF : PER;
   __shared__ float2 tw[kN];
   __shared__ __attribute__((aligned(16))) float2 tile[kSCR];
   __shared__ double red[kGPB][3];
@@ -299,9 +313,11 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
   const float2* jbase = ws_b + (size_t)j * P * kPlaneB;
   const int k1 = t < kL ? t : 0;
 
-  float4 pre[PER];   // this thread's share of a plane tile, one plane ahead
+  // this thread's share of a plane tile: PF chunks prefetched one plane ahead
+  // in registers, the rest loaded when the tile is written (register budget)
+  float4 pre[PF];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
+  for (int i = 0; i < PF; ++i) {
     const int c = threadIdx.x + 256 * i;
     const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
     pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * kN + y0 + r2);
@@ -313,17 +329,28 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
 #pragma unroll 1
   for (int p = 0; p < P; ++p) {
     lds_barrier();  // previous plane's scratch use is over (also publishes tw)
+    {
+      const float2* cb = jbase + (size_t)p * kPlaneB;
+      float4 late[PER - PF > 0 ? PER - PF : 1];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = threadIdx.x + 256 * i;
-      const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-      tile[tile_pos<kR, kGPB>(line, r2)] = make_float2(pre[i].x, pre[i].y);
-      tile[tile_pos<kR, kGPB>(line, r2 + 1)] = make_float2(pre[i].z, pre[i].w);
+      for (int i = PF; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
+        late[i - PF] = *reinterpret_cast<const float4*>(cb + (size_t)line * kN + y0 + r2);
+      }
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
+        const float4 q = i < PF ? pre[i] : late[i - PF];
+        tile[tile_pos<kR, kGPB>(line, r2)] = make_float2(q.x, q.y);
+        tile[tile_pos<kR, kGPB>(line, r2 + 1)] = make_float2(q.z, q.w);
+      }
     }
     if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
       const float2* nb = jbase + (size_t)(p + 1) * kPlaneB;
 #pragma unroll
-      for (int i = 0; i < PER; ++i) {
+      for (int i = 0; i < PF; ++i) {
         const int c = threadIdx.x + 256 * i;
         const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
         pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * kN + y0 + r2);
@@ -334,7 +361,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
 #pragma unroll
     for (int k2 = 0; k2 < 32; ++k2) v[k2] = tile[tile_pos<kR, kGPB>(k1 + kL * k2, grp)];
     lds_barrier();  // tile consumed: reuse it as transpose scratch
-    fft896_sn<true>(v, t, PaddedScratch<kR>{tile + grp * kR * (kR + 1)}, tw);
+    fft896_sn<true, kInvScalar>(v, t, PaddedScratch<kR>{tile + grp * kR * (kR + 1)}, tw);
 #pragma unroll
     for (int k = 0; k < kL; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
     if (field_out) {  // exact field of this plane (incremental mode init / refresh)
