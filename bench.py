@@ -239,11 +239,11 @@ def psnr_check(vec, N):
     return abs(prop.psnr(st) - float(vec.state.init_psnr[0].item()))
 
 
-def load_pmc_traffic():
+def load_pmc_traffic(N: int = 1024):
     """Per-launch HBM bytes of the dominant kernels from the committed rocprofv3
     PMC summary (profiles/pmc_latest.json, written by tools/pmc_summary.py from
     separate FETCH_SIZE / WRITE_SIZE passes with the gfx950 x2 read correction)."""
-    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json" if N == 1024 else f"pmc_latest_{N}.json")
     if not os.path.exists(p):
         return None
     try:
@@ -335,7 +335,7 @@ def main():
     if rank == 0:
         dom = max(passes, key=lambda n: passes[n]["avg_ms"])
         d = passes[dom]
-        pmc = load_pmc_traffic()
+        pmc = load_pmc_traffic(N)
         traffic = None
         if pmc and dom in pmc.get("kernels", {}):
             kinfo = pmc["kernels"][dom]
@@ -348,7 +348,8 @@ def main():
                                                              "k_colbits")) * B
         canon = canonical_step_bytes(N, P)
         out = {
-            "metric": "env-steps/sec (1024x1024, 24-plane)",
+            "metric": "env-steps/sec (1024x1024, 24-plane)" if N == 1024 else
+                      f"env-steps/sec ({N}x{N} crop of 1024x1024, 24-plane)",
             "value": round(value, 2),
             "unit": "env-steps/s",
             "n_gpus": world,
