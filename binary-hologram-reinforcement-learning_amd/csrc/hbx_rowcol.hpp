@@ -21,6 +21,13 @@ __device__ __forceinline__ int tile_pos(int line, int r) {
     // line -- conflict-free for the lane-row reads / writes and the 16-B chunk
     // writes; the chunk reads of k_rowfwd stay 2-way (checked exhaustively)
     return line * GPB + (r ^ (((line & 15) ^ ((line >> 4) & 1)) & (GPB - 1)));
+  } else if constexpr (R == 32 && GPB == 8) {
+    // q ^ 5 b1 (q = bits 2-4 of line, b1 = bit 1): the lane-row reads stay
+    // conflict-free (bijective in q for fixed line mod 4) and the two b64
+    // writes -- lane rows t + 32 k2 (16-lane groups: bijective in bits 1-3)
+    // and the 16-B chunk pairs of 4 consecutive lines (the b1 term flips the
+    // parity) -- lose their 2-way conflicts (tools/lds_swizzle_model.py)
+    return line * GPB + (r ^ ((((line & 31) >> 2) ^ (((line >> 1) & 1) * 5)) & 7));
   } else {
     constexpr int SR = ilog2c(32 / GPB);
     constexpr int SL = ilog2c(GPB / 8);
