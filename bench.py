@@ -55,6 +55,7 @@ def parse():
                          "SURVEY 8d cfg 2 (0 = skip)")
     ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")
     ap.add_argument("--no-probe", action="store_true", help="skip the all-flip probe-sweep measurement")
+    ap.add_argument("--no-ppo", action="store_true", help="skip the 256x256x8 mono (train-PPO) measurement")
     return ap.parse_args()
 
 
@@ -274,7 +275,7 @@ def main():
     import torch
     from hbx import dist as hd
     from hbx.env import HologramVecEnv
-    from hbx.plan import rgb_config
+    from hbx.plan import mono_config, rgb_config
 
     rank, world, local = hd.init()
     if world != args.gpus and rank == 0:
@@ -295,14 +296,23 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i))
         return torch.rand((CH, N, N), generator=g, device="cuda")
 
-    def measure(mode: str, steps: int, warmup: int):
-        vec = HologramVecEnv(cfg, B, target_source, pre_model_source=pre_model_source, obs_keys=(),
+    def measure(mode: str, steps: int, warmup: int, mcfg=None):
+        mcfg = mcfg or cfg
+        mG, mCH, mN = mcfg.groups, mcfg.channels, mcfg.height
+
+        def tsrc(i):
+            return target_source(i)[:mG, :mN, :mN].contiguous()
+
+        def psrc(i):
+            return pre_model_source(i)[:mCH, :mN, :mN].contiguous()
+
+        vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=(),
                              auto_reset=False, max_steps=10 ** 9, max_jobs=args.chunk or None, mode=mode,
                              refresh_every=0)
         vec.reset()
         gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
         total = warmup + steps
-        actions = torch.randint(0, CH * N * N, (total, B), generator=gen, device="cuda", dtype=torch.int64)
+        actions = torch.randint(0, mCH * mN * mN, (total, B), generator=gen, device="cuda", dtype=torch.int64)
 
         def one_step(k):
             r, ps, acc, term, trunc = vec.step_device(actions[k])
@@ -407,6 +417,20 @@ def main():
                 "passes": rounded(ps),
                 "note": "same env semantics; a flip adds +-h_g(shifted) to the touched plane's cached field "
                         "(linearity of the propagation), no FFT per step; reported separately per SURVEY 8d"}
+        vec.close()
+
+    if world == 1 and not args.no_ppo:
+        # SURVEY 3.2 / BASELINE cfg 4's per-GPU shard: train-PPO.py's env (env.py, 256x256x8 mono),
+        # 128 envs per GPU, FFT mode -- a secondary line, not the headline metric
+        mono = mono_config(256)
+        vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup, mcfg=mono)
+        ps = pass_table(timing, algorithmic_bytes(256, mono.planes))
+        out["ppo_mono_256"] = {
+            "value": round(B * args.steps / dt, 2), "unit": "env-steps/s", "envs": B,
+            "ms_per_step": round(dt / args.steps * 1e3, 4), "accept_rate": round(acc_rate, 4),
+            "passes": rounded(ps),
+            "note": "env.py / train-PPO.py configuration (256x256, 1 colour group x 8 planes at 515 nm), "
+                    "FFT mode, same env semantics as the headline"}
         vec.close()
 
     if rank == 0:

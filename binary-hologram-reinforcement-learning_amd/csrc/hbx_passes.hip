@@ -277,7 +277,11 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #else
 #define COL2_H(k2) buf_ld2(rh, vh, (k2) * R * 8)
 #endif
+#ifdef HBX_COL2_FWD_PACKED   // A/B switch: packed DFTs for the forward FFT only (one line live)
+    fft_group<R, false, false>(v, t, sc, tw);
+#else
     fft_group<R, false, HBX_COL2_SCALAR>(v, t, sc, tw);
+#endif
     // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
     // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
     // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
