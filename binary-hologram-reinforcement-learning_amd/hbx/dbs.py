@@ -85,7 +85,7 @@ def walk_k(q: float, n: int, k_min: int = 1, k_max: int = 256) -> int:
 
 
 def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream,
-                 refresh_every, chunk: int = 64) -> GreedyResult:
+                 refresh_every, chunk: int = 64, progress=None) -> GreedyResult:
     """greedy(mode="psf") on the device-resident walk (hbx_dbs_walk_psf).
 
     The host keeps two chunks of `chunk` batches in flight: chunk n+1 is
@@ -147,6 +147,8 @@ def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_m
     while True:
         st = take()
         marks.append((int(st.accepted), time.perf_counter() - t0))
+        if progress is not None:
+            progress(int(st.pos), int(st.accepted), float(st.prev_psnr), marks[-1][1])
         dpos, dacc = st.pos - pos_prev, st.accepted - acc_prev
         if dpos > 0:
             q = 0.5 * q + 0.5 * (dacc / dpos)
@@ -196,7 +198,7 @@ def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_m
 
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
-           stream=None, mode: str = "fft", refresh_every: int = 4096) -> GreedyResult:
+           stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
     mode="fft": every candidate is a full propagation of its colour group.
@@ -204,7 +206,9 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     whole walk device-resident (hbx_dbs_walk_psf); the base fields are
     re-propagated exactly every ``refresh_every`` accepted flips.
     mode="psf_host": the same candidates through hbx_eval_flips_psf /
-    hbx_commit_flip_psf with a host decision per batch."""
+    hbx_commit_flip_psf with a host decision per batch.
+    progress(pos, accepted, prev_psnr, seconds): optional callback per chunk of
+    the device walk (mode="psf")."""
     if mode not in ("fft", "psf", "psf_host"):
         raise ValueError(f"mode must be 'fft', 'psf' or 'psf_host', got {mode!r}")
     dev = plan.device
@@ -212,7 +216,7 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
         total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
         return _greedy_walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
-                            stream, refresh_every)
+                            stream, refresh_every, progress=progress)
     mode = "psf" if mode == "psf_host" else mode
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
