@@ -176,8 +176,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
     const float2 b = store_round(tile[tile_pos<R, GPB>(line, r2 + 1)]);
     const int pl = line / (N / 2);
     // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
-    *reinterpret_cast<float4*>(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2)) =
-        make_float4(a.x, a.y, b.x, b.y);
+    st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),
+               make_float4(a.x, a.y, b.x, b.y));
   }
 }
 
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   {
     const int vo = PA::voff(t, kx0);
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2(ra, vo, PA::joff(jj)));
+    for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2s(ra, vo, PA::joff(jj)));
   }
   lds_barrier();  // tw visible (the line loads stay in flight)
 
@@ -325,18 +325,18 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     {
       const int vo = PB::voff(t, kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2(store_round(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
     }
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
       const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2(ra, vo, PA::joff(jj)));
+      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2s(ra, vo, PA::joff(jj)));
     }
     fft_group<R, true, HBX_COL2_SCALAR>(m, t, sc, tw);
     {
       const int vo = PB::voff(t, dc ? N / 2 : N - kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2(store_round(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
     }
   }
 #undef COL2_H
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
   for (int i = 0; i < PER; ++i) {
     const int c = threadIdx.x + NT * i;
     const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-    pre[i] = *reinterpret_cast<const float4*>(jbase + LayoutB<R>::at(line, y0 + r2));
+    pre[i] = ld_stream4(jbase + LayoutB<R>::at(line, y0 + r2));
   }
   float acc[R];
 #pragma unroll
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
       for (int i = 0; i < PER; ++i) {
         const int c = threadIdx.x + NT * i;
         const int line = c / (GPB / 2), r2 = (c % (GPB / 2)) * 2;
-        pre[i] = *reinterpret_cast<const float4*>(nb + LayoutB<R>::at(line, y0 + r2));
+        pre[i] = ld_stream4(nb + LayoutB<R>::at(line, y0 + r2));
       }
     }
     lds_barrier();

@@ -147,8 +147,8 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd896(const JobDesc* __restrict_
     const float2 a = tile[tile_pos<kR, kGPB>(line, r2)];
     const float2 b = tile[tile_pos<kR, kGPB>(line, r2 + 1)];
     const int pl = line / kHalf;
-    *reinterpret_cast<float4*>(base + (size_t)pl * kPlaneA + (size_t)(line - pl * kHalf) * kN + y0 + r2) =
-        make_float4(a.x, a.y, b.x, b.y);
+    st_stream4(base + (size_t)pl * kPlaneA + (size_t)(line - pl * kHalf) * kN + y0 + r2,
+               make_float4(a.x, a.y, b.x, b.y));
   }
 }
 
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
   {
     const int vo = (kx0 * kN + t) * 8;
 #pragma unroll
-    for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2(ra, vo, jj * kR * 8);
+    for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, vo, jj * kR * 8);
 #pragma unroll
     for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
   }
@@ -255,12 +255,12 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     {
       const int vo = (kx * kN + t) * 8;
 #pragma unroll
-      for (int jj = 0; jj < kL; ++jj) buf_st2(v[jj], rb, vo, jj * kR * 8);
+      for (int jj = 0; jj < kL; ++jj) buf_st2s(v[jj], rb, vo, jj * kR * 8);
     }
     if (it + 1 < kColIter) {  // next line in flight under the second inverse FFT
       const int vo = ((kx + KSTEP) * kN + t) * 8;
 #pragma unroll
-      for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2(ra, vo, jj * kR * 8);
+      for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, vo, jj * kR * 8);
 #pragma unroll
       for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
     }
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     {
       const int vo = ((dc ? kHalf : kN - kx) * kN + t) * 8;
 #pragma unroll
-      for (int jj = 0; jj < kL; ++jj) buf_st2(m[jj], rb, vo, jj * kR * 8);
+      for (int jj = 0; jj < kL; ++jj) buf_st2s(m[jj], rb, vo, jj * kR * 8);
     }
   }
 }
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
   for (int i = 0; i < PF; ++i) {
     const int c = threadIdx.x + 256 * i;
     const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-    pre[i] = *reinterpret_cast<const float4*>(jbase + (size_t)line * kN + y0 + r2);
+    pre[i] = ld_stream4(jbase + (size_t)line * kN + y0 + r2);
   }
   float acc[kL];
 #pragma unroll
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
       for (int i = PF; i < PER; ++i) {
         const int c = threadIdx.x + 256 * i;
         const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-        late[i - PF] = *reinterpret_cast<const float4*>(cb + (size_t)line * kN + y0 + r2);
+        late[i - PF] = ld_stream4(cb + (size_t)line * kN + y0 + r2);
       }
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
       for (int i = 0; i < PF; ++i) {
         const int c = threadIdx.x + 256 * i;
         const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-        pre[i] = *reinterpret_cast<const float4*>(nb + (size_t)line * kN + y0 + r2);
+        pre[i] = ld_stream4(nb + (size_t)line * kN + y0 + r2);
       }
     }
     lds_barrier();

@@ -54,6 +54,44 @@ __device__ __forceinline__ void buf_st2(float2 v, __amdgpu_buffer_rsrc_t rs, int
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
 
+// Cache policy of the once-touched intermediate streams (A, B): timing switches
+// HBX_NT_LOADS / HBX_NT_STORES set the non-temporal bit (buffer aux = 2,
+// `__builtin_nontemporal_*` for flat accesses).
+#ifdef HBX_NT_LOADS
+constexpr int kLdAux = 2;
+#else
+constexpr int kLdAux = 0;
+#endif
+#ifdef HBX_NT_STORES
+constexpr int kStAux = 2;
+#else
+constexpr int kStAux = 0;
+#endif
+__device__ __forceinline__ float2 buf_ld2s(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, kLdAux));
+}
+__device__ __forceinline__ void buf_st2s(float2 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, kStAux);
+}
+__device__ __forceinline__ float4 ld_stream4(const float2* p) {
+#ifdef HBX_NT_LOADS
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ void st_stream4(float2* p, float4 v) {
+#ifdef HBX_NT_STORES
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 // Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
 // the 8 XCDs; placement is a speed hint only, never relied on for
 // correctness).  The row passes touch 64-B pieces of every 8-KB line, the
