@@ -378,6 +378,8 @@ class ProbeResult:
     attempted_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.int64))
     improved_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.int64))
     delta_bins: np.ndarray = field(default_factory=lambda: np.zeros(10, np.float64))
+    shard: Optional[tuple] = None            # probe_sharded: this rank's [lo, hi) of the flips
+    improved_total: Optional[int] = None     # probe_sharded: improved flips over all ranks
 
 
 def premodel_bins(values: np.ndarray) -> np.ndarray:
@@ -415,6 +417,41 @@ def probe(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips, pre_model
             res.attempted_bins[i] = int(sel.sum())
             res.improved_bins[i] = int((sel & improved).sum())
             res.delta_bins[i] = float(np.sum((ps - base)[sel & improved]))
+    return res
+
+
+def probe_sharded(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips, pre_model=None,
+                  stream=None) -> ProbeResult:
+    """The probe sweep of DBS_1024_24-128.py:310-373 / range.py:294-335 split across
+    the ranks of the default process group: rank r evaluates its
+    contiguous share of `flips` (hbx.dist.shard_range) against the same fixed
+    base, then the 10-bin pre-model histogram (attempted, improved, summed
+    PSNR gain) and the improved count are all-reduced (RCCL over xGMI on GPUs,
+    gloo on CPU) -- the only exchange.  Returns the global histogram on every
+    rank; `psnr` / `improved` hold this rank's share (positions lo..hi of
+    `flips`, given by the returned `.shard`)."""
+    from . import dist as hd
+    flips = np.asarray(flips, np.int64)
+    rank, world = 0, 1
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
+    lo, hi = hd.shard_range(len(flips), rank, world)
+    res = probe(plan, mask, target, flips[lo:hi], pre_model=pre_model, stream=stream)
+    # histogram rows + improved count in one f64 all-reduce (device of the collective's backend)
+    backend = torch.distributed.get_backend() if world > 1 else "gloo"
+    dev = plan.device if backend == "nccl" else torch.device("cpu")
+    buf = torch.zeros(31, dtype=torch.float64, device=dev)
+    buf[0:10] = torch.as_tensor(res.attempted_bins, dtype=torch.float64)
+    buf[10:20] = torch.as_tensor(res.improved_bins, dtype=torch.float64)
+    buf[20:30] = torch.as_tensor(res.delta_bins, dtype=torch.float64)
+    buf[30] = float(np.count_nonzero(res.improved))
+    hd.allreduce_hist(buf)
+    out = buf.cpu().numpy()
+    res.attempted_bins = out[0:10].round().astype(np.int64)
+    res.improved_bins = out[10:20].round().astype(np.int64)
+    res.delta_bins = out[20:30].copy()
+    res.shard = (lo, hi)
+    res.improved_total = int(round(out[30]))
     return res
 
 

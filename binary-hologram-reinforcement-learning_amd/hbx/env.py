@@ -310,6 +310,38 @@ class HologramVecEnv:
                 out[k] = rec.unsqueeze(1)
         return out
 
+    # -- checkpoint / resume (the env state is plain tensors) ---------------
+    _SNAPSHOT = ("mask", "record", "target", "pre_model", "intensity", "chan_stats", "init_psnr",
+                 "prev_psnr", "max_psnr_diff", "steps", "flip_count", "sustained", "imp_changes",
+                 "imp_values", "t_psnr_diff")
+
+    def save(self, path: str):
+        """Every env's device state to an .npz (bit-packed masks, records, targets,
+        pre-model, channel statistics, PSNR history, counters, importance tables)
+        -- the resume point the reference keeps outside the env (train-PPO.py:285-291
+        learner zips, DBS_1024_24.py:282-287 recon arrays).  No pickles: load() reads
+        it back with numpy's default allow_pickle=False."""
+        c, st = self.cfg, self.state
+        arrs = {k: getattr(st, k).detach().cpu().numpy() for k in self._SNAPSHOT if getattr(st, k) is not None}
+        arrs["meta"] = np.array([c.height, c.width, c.groups, c.planes, self.num_envs], np.int64)
+        np.savez(path, **arrs)
+
+    def load(self, path: str):
+        """Restore a save() of an env with the same shape; incremental mode
+        re-propagates the cached fields of the restored masks exactly."""
+        c, st = self.cfg, self.state
+        with np.load(path) as z:
+            meta = tuple(int(v) for v in z["meta"])
+            if meta != (c.height, c.width, c.groups, c.planes, self.num_envs):
+                raise ValueError(f"snapshot shape {meta} does not match this env "
+                                 f"{(c.height, c.width, c.groups, c.planes, self.num_envs)}")
+            for k in self._SNAPSHOT:
+                t = getattr(st, k)
+                if t is not None and k in z.files:
+                    t.copy_(torch.from_numpy(z[k]))
+        if self.mode == "psf":
+            self.refresh()
+
     # -- gym-ish accessors ------------------------------------------------------------
     @property
     def initial_psnr(self):

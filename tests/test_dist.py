@@ -61,3 +61,49 @@ def test_gloo_world2_gather_and_reduce():
     assert len(g) == 8                       # 4 envs x 2 ranks, rank order
     assert g[0][0] == 0.0 and g[4][0] == 100.0 and g[5][1] == 11.0 and g[4][4] == 1.0
     assert hist == [3, 2] and mx == 1.5 and (lo, hi) == (0, 512)
+
+
+def _probe_worker(rank, world, port, out):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "binary-hologram-reinforcement-learning_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from hbx import dbs
+    from hbx import dist as hd
+    from tests._probe_fake import OraclePlan, probe_inputs
+    hd.init(backend="gloo")
+    ocfg, pre, tgt, mask, flips = probe_inputs()
+    res = dbs.probe_sharded(OraclePlan(ocfg), mask, tgt, flips, pre_model=pre)
+    out.put((rank, res.shard, res.attempted_bins.tolist(), res.improved_bins.tolist(),
+             res.delta_bins.tolist(), res.improved_total, res.psnr.tolist()))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_gloo_world2_sharded_probe_sweep():
+    """the probe sweep's flip range split over 2 ranks, the 10-bin
+    pre-model histogram all-reduced -- equals the single-process probe over
+    all flips (propagation answered by the oracle: tests/_probe_fake.py)."""
+    import numpy as np
+    from hbx import dbs
+    from tests._probe_fake import OraclePlan, probe_inputs
+    ocfg, pre, tgt, mask, flips = probe_inputs()
+    want = dbs.probe(OraclePlan(ocfg), mask, tgt, flips, pre_model=pre)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_probe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0][1] == (0, 45) and res[1][1] == (45, 90)
+    for r in res:
+        assert r[2] == want.attempted_bins.tolist()
+        assert r[3] == want.improved_bins.tolist()
+        assert np.allclose(r[4], want.delta_bins, rtol=1e-12, atol=1e-15)
+        assert r[5] == int(np.count_nonzero(want.improved))
+    assert np.allclose(res[0][6] + res[1][6], want.psnr, rtol=0, atol=1e-12)

@@ -308,6 +308,42 @@ def test_vecenv_auto_reset_and_obs():
     assert seen_done
 
 
+@pytest.mark.parametrize("mode", ["fft", "psf"])
+def test_vecenv_save_load_resume(tmp_path, mode):
+    """HologramVecEnv.save / load: a restored env continues bit-identically."""
+    from hbx.env import HologramVecEnv
+    cfg = dev_cfg(small_rgb())
+    B = 3
+    gens = [torch.Generator(device="cuda").manual_seed(40 + i) for i in range(B)]
+    pres = [torch.rand((cfg.channels, 64, 64), generator=g, device="cuda") for g in gens]
+    tgts = [torch.rand((cfg.groups, 64, 64), generator=g, device="cuda") for g in gens]
+    keys = ("state_record", "state") if mode == "psf" else ("state_record", "state", "recon_image")
+    kw = dict(pre_model_source=lambda i: pres[i], obs_keys=keys, auto_reset=False, mode=mode, refresh_every=0)
+    a = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    a.reset()
+    acts = torch.randint(0, cfg.channels * 64 * 64, (24, B), generator=gens[0], device="cuda")
+    for k in range(12):
+        a.step_device(acts[k])
+    if mode == "psf":
+        a.refresh()
+    path = str(tmp_path / "env.npz")
+    a.save(path)
+    b = HologramVecEnv(cfg, B, lambda i: tgts[(i + 1) % B], **kw)
+    b.reset()
+    b.load(path)
+    for k in range(12, 24):
+        ra, rb = a.step_device(acts[k]), b.step_device(acts[k])
+        for x, y in zip(ra, rb):
+            assert torch.equal(x, y)
+    for name in ("mask", "record", "chan_stats", "steps", "flip_count", "prev_psnr"):
+        assert torch.equal(getattr(a.state, name), getattr(b.state, name)), name
+    c = HologramVecEnv(cfg, B + 1, lambda i: tgts[0], **kw)
+    with pytest.raises(ValueError):
+        c.load(path)
+    for e in (a, b, c):
+        e.close()
+
+
 # -- DBS --------------------------------------------------------------------------------------
 def test_dbs_greedy_speculative_equals_serial(golden_dir):
     import hbx
