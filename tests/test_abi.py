@@ -80,3 +80,28 @@ def test_product_path_fails_loudly_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(ImportError):
         L.load()
+
+
+def test_abi_error_paths_under_asan(tmp_path):
+    """SURVEY 5 (sanitizers on host code only): the C-ABI's argument validation,
+    null-plan handling and device-selection failure, exercised from C against
+    libhbx_asan.so (host code AddressSanitizer-instrumented; csrc/Makefile
+    `asan`).  No GPU needed: nothing reaches a kernel launch."""
+    import shutil
+    clang = "/opt/rocm/lib/llvm/bin/clang"
+    if not os.path.exists(clang):
+        pytest.skip("ROCm clang not present")
+    csrc = os.path.join(ROOT, "binary-hologram-reinforcement-learning_amd", "csrc")
+    hbxdir = os.path.join(ROOT, "binary-hologram-reinforcement-learning_amd", "hbx")
+    if shutil.which("make") is None:
+        pytest.skip("make not present")
+    subprocess.run(["make", "-C", csrc, "asan", f"-j{min(8, os.cpu_count() or 2)}"], check=True,
+                   capture_output=True, timeout=600)
+    exe = str(tmp_path / "abi_errors")
+    subprocess.run([clang, "-fsanitize=address", "-fno-omit-frame-pointer", "-g",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "c", "abi_errors.c"),
+                    "-L", hbxdir, "-lhbx_asan", f"-Wl,-rpath,{hbxdir}", "-o", exe], check=True, timeout=120)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+    assert "AddressSanitizer" not in r.stderr, r.stderr
