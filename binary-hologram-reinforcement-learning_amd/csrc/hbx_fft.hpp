@@ -547,6 +547,61 @@ __device__ __forceinline__ void dft28(float2 (&v)[32]) {
   }
 }
 
+// Packed-f32 variants (two floats per VALU op: v_pk_add / v_pk_fma with a
+// broadcast constant): half the VALU of the scalar radix-4 / radix-7 stages.
+__device__ __forceinline__ pk2 pk_mul_mi(pk2 a) { return (pk2){a.y, -a.x}; }   // a * (-i)
+__device__ __forceinline__ pk2 pk_mul_pi(pk2 a) { return (pk2){-a.y, a.x}; }   // a * (+i)
+
+template <bool INV>
+__device__ __forceinline__ void dft7_pk(pk2 (&x)[7]) {
+  pk2 a[4], b[4];
+#pragma unroll
+  for (int m = 1; m <= 3; ++m) { a[m] = x[m] + x[7 - m]; b[m] = x[m] - x[7 - m]; }
+  const pk2 x0 = x[0];
+  x[0] = x0 + (a[1] + (a[2] + a[3]));
+#pragma unroll
+  for (int k = 1; k <= 3; ++k) {
+    pk2 u = x0, w = (pk2){0.f, 0.f};
+#pragma unroll
+    for (int m = 1; m <= 3; ++m) {
+      const float c = c7(m * k), sn = s7(m * k);
+      u = __builtin_elementwise_fma((pk2){c, c}, a[m], u);
+      w = __builtin_elementwise_fma((pk2){sn, sn}, b[m], w);
+    }
+    const pk2 miw = pk_mul_mi(w);
+    x[k] = INV ? u - miw : u + miw;
+    x[7 - k] = INV ? u + miw : u - miw;
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4_pk(pk2& x0, pk2& x1, pk2& x2, pk2& x3) {
+  const pk2 t0 = x0 + x2, t1 = x0 - x2, t2 = x1 + x3, t3 = x1 - x3;
+  const pk2 mi3 = INV ? pk_mul_pi(t3) : pk_mul_mi(t3);
+  x0 = t0 + t2;
+  x2 = t0 - t2;
+  x1 = t1 + mi3;
+  x3 = t1 - mi3;
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft28_pk(float2 (&v)[32]) {
+  pk2 y[4][7];
+#pragma unroll
+  for (int n2 = 0; n2 < 7; ++n2) {
+    pk2 e0 = to_pk(v[(4 * n2) % 28]), e1 = to_pk(v[(7 + 4 * n2) % 28]);
+    pk2 e2 = to_pk(v[(14 + 4 * n2) % 28]), e3 = to_pk(v[(21 + 4 * n2) % 28]);
+    dft4_pk<INV>(e0, e1, e2, e3);
+    y[0][n2] = e0; y[1][n2] = e1; y[2][n2] = e2; y[3][n2] = e3;
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    dft7_pk<INV>(y[k1]);
+#pragma unroll
+    for (int k2 = 0; k2 < 7; ++k2) v[(21 * k1 + 8 * k2) % 28] = from_pk(y[k1][k2]);
+  }
+}
+
 // 896-point FFT by 32 lanes, natural layout in -> slot layout out.
 // tw896: LDS [k1 < 28][t < 32] = W896^{t k1} (forward sign); INV conjugates.
 // SCALAR: scalar-f32 32-point DFTs (fewer live registers than the packed ones
@@ -554,11 +609,20 @@ __device__ __forceinline__ void dft28(float2 (&v)[32]) {
 template <bool INV, bool SCALAR = false, class Scratch>
 __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
   asm volatile("" ::: "memory");
-  dft28<INV>(v);
+  if constexpr (SCALAR) {
+    dft28<INV>(v);
 #pragma unroll
-  for (int k1 = 1; k1 < 28; ++k1) {
-    const float2 w = tw896[k1 * 32 + t];
-    v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    for (int k1 = 1; k1 < 28; ++k1) {
+      const float2 w = tw896[k1 * 32 + t];
+      v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    }
+  } else {
+    dft28_pk<INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 28; ++k1) {
+      const pk2 w = to_pk(tw896[k1 * 32 + t]);
+      v[k1] = from_pk(INV ? pk_cmulc(to_pk(v[k1]), w) : pk_cmul(to_pk(v[k1]), w));
+    }
   }
   wave_sync();
 #pragma unroll
@@ -590,12 +654,21 @@ __device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch&
 #pragma unroll
   for (int k1 = 0; k1 < 28; ++k1) v[k1] = *sc.at(t, k1);
   wave_sync();
+  if constexpr (SCALAR) {
 #pragma unroll
-  for (int k1 = 1; k1 < 28; ++k1) {
-    const float2 w = tw896[k1 * 32 + t];
-    v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    for (int k1 = 1; k1 < 28; ++k1) {
+      const float2 w = tw896[k1 * 32 + t];
+      v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    }
+    dft28<INV>(v);              // over k1 -> register j: x[t + 32 j]
+  } else {
+#pragma unroll
+    for (int k1 = 1; k1 < 28; ++k1) {
+      const pk2 w = to_pk(tw896[k1 * 32 + t]);
+      v[k1] = from_pk(INV ? pk_cmulc(to_pk(v[k1]), w) : pk_cmul(to_pk(v[k1]), w));
+    }
+    dft28_pk<INV>(v);
   }
-  dft28<INV>(v);              // over k1 -> register j: x[t + 32 j]
 }
 
 }  // namespace hbx
