@@ -278,6 +278,44 @@ def test_vecenv_batch_matches_oracle_per_env():
             assert bool(acc[b]) == want.accepted
 
 
+@pytest.mark.parametrize("size,mono", [(1024, False), (256, True)])
+def test_env_steps_full_size_vs_oracle(size, mono):
+    """The headline configuration (1024x1024x24 RGB) and env.py's 256x256x8 mono:
+    per-step PSNR and reward against the float64 oracle evaluated on the SAME
+    state (the oracle follows the GPU's accept decisions), and the decisions
+    themselves wherever the PSNR change is clear of fp32 resolution (1e-5 dB;
+    a single flip moves the 1024x24 PSNR by ~1e-6 dB, below what an f32 field
+    can order against an f64 reference)."""
+    from hbx.env import HologramVecEnv
+    ocfg = O.mono_config(size) if mono else O.rgb_config(size)
+    pre, tgt = O.synthetic_inputs(ocfg, 3)
+    env = HologramVecEnv(dev_cfg(ocfg), 1, lambda i: tgt, pre_model_source=lambda i: pre, auto_reset=False,
+                         obs_keys=())
+    env.reset()
+    oe = O.OracleEnv(ocfg)
+    oe.reset(pre, tgt)
+    assert abs(float(env.state.init_psnr[0]) - oe.initial_psnr) <= PSNR_TOL
+    rng = np.random.default_rng(4)
+    clear = 0
+    for _ in range(8):
+        a = int(rng.integers(0, ocfg.channels * size * size))
+        r, ps, acc, _, _ = env.step_device(torch.tensor([a], device="cuda"))
+        want, g, ig, st = oe.evaluate_flip(a)
+        change = want - oe.previous_psnr
+        assert abs(float(ps[0]) - want) <= PSNR_TOL
+        assert abs(float(r[0]) - O.RW * change) <= O.RW * 2 * PSNR_TOL
+        if abs(change) > 1e-5:
+            clear += 1
+            assert bool(acc[0]) == (change >= 0)
+        if bool(acc[0]):                       # follow the GPU's decision
+            ch, row, col = (int(v) for v in O.decode_action(a, size, size))
+            oe.state[ch, row, col] ^= 1
+            oe.stats, oe.intensity[g], oe.previous_psnr = st, ig, want
+    assert torch.equal(env.state.mask[0].cpu(), torch.from_numpy(O.pack_mask(oe.state.astype(np.uint8)).view(np.int64)))
+    if mono:
+        assert clear > 0
+
+
 def test_invalid_action_raises():
     from hbx.env import HologramVecEnv
     ocfg = small_rgb()
