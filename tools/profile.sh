@@ -9,6 +9,9 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 BENCH="python3 bench.py --steps 6 --warmup 2 --psf-steps 20 --cpu-sample 0 --dbs-flips 0 --no-probe --no-psnr-check $*"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1 || exit 1
+# headline-only trace: every FFT-mode pass launch is a 128-job step / reset chunk, so the
+# --stats average of the dominant kernel is directly comparable with bench.py's roofline
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_headline -o run -- $BENCH --no-psf --no-ppo > $OUT/trace_headline.log 2>&1 || exit 6
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $BENCH > $OUT/fetch.log 2>&1 || exit 2
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $BENCH > $OUT/write.log 2>&1 || exit 3
 timeout -k 10 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $OUT/sq -o run -- $BENCH > $OUT/sq.log 2>&1 || exit 4
