@@ -98,9 +98,10 @@ __global__ __launch_bounds__(256) void k_bits_t(const JobDesc* __restrict__ jobs
     uint32_t x = src[(size_t)y * 32 + n1];
     if (flip_here && fy == y && (fx >> 5) == n1) x ^= 1u << (fx & 31);   // env.py:164
 #pragma unroll
-    for (int s = 16; s >= 1; s >>= 1) {
-      const uint32_t m = s == 16 ? 0x0000FFFFu : s == 8 ? 0x00FF00FFu : s == 4 ? 0x0F0F0F0Fu
-                       : s == 2 ? 0x33333333u : 0x55555555u;
+    for (int st = 0; st < 5; ++st) {
+      const int s = 16 >> st;
+      const uint32_t m = st == 0 ? 0x0000FFFFu : st == 1 ? 0x00FF00FFu : st == 2 ? 0x0F0F0F0Fu
+                       : st == 3 ? 0x33333333u : 0x55555555u;
       const uint32_t q = (uint32_t)__shfl_xor((int)x, s, 64);
       x = (n1 & s) ? ((x & ~m) | ((q >> s) & m)) : ((x & m) | ((q & m) << s));
     }

@@ -706,6 +706,40 @@ def test_dbs_walk_early_stop_and_prefix():
     assert all(p < 777 for p in res.accepted_positions)
 
 
+def test_dbs_greedy_many_equals_single_walks():
+    """dbs.greedy_many (several images' walks side by side, one stream each)
+    returns exactly what greedy(mode="psf") returns for each image alone,
+    including a walk that halts for exact refreshes and one that stops early."""
+    import hbx
+    from hbx import dbs
+    ocfg = small_rgb()
+    cfg = dev_cfg(ocfg)
+    n = ocfg.channels * 64 * 64
+    ins = [O.synthetic_inputs(ocfg, 60 + i) for i in range(3)]
+    orders = [np.random.default_rng(70 + i).permutation(n)[:3000] for i in range(3)]
+    masks = [hbx.pack_bits(torch.from_numpy(p).cuda() >= 0.5) for p, _ in ins]
+    tgts = [torch.from_numpy(t).cuda() for _, t in ins]
+    single = []
+    for i in range(3):
+        plan = hbx.Plan(cfg, max_jobs=cfg.groups)
+        m = masks[i].clone()
+        single.append((dbs.greedy(plan, m, tgts[i], orders[i], mode="psf", refresh_every=256), m))
+        plan.close()
+    plans = [hbx.Plan(cfg, max_jobs=cfg.groups) for _ in range(3)]
+    ms = [m.clone() for m in masks]
+    many = dbs.greedy_many(plans, ms, tgts, orders, refresh_every=256)
+    for (want, wm), got, gm in zip(single, many, ms):
+        assert got.accepted_positions == want.accepted_positions
+        assert got.final_psnr == want.final_psnr and got.steps == want.steps
+        assert torch.equal(gm, wm)
+    stop = dbs.greedy_many(plans[:2], [m.clone() for m in masks[:2]], tgts[:2], orders[:2], stop_diff=0.02)
+    for i, r in enumerate(stop):
+        w = dbs.greedy(plans[i], masks[i].clone(), tgts[i], orders[i], mode="psf", stop_diff=0.02)
+        assert r.stopped_early == w.stopped_early and r.accepted_positions == w.accepted_positions
+    for p in plans:
+        p.close()
+
+
 @pytest.mark.parametrize("field_kind", [0, 1])
 def test_dbs_walk_matches_host_batches_1024(field_kind):
     """1024 x 24 RGB: the device-resident walk and the host-decided psf batches

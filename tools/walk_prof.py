@@ -15,11 +15,27 @@ from hbx import dbs  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 mode = sys.argv[2] if len(sys.argv) > 2 else "psf"
+many = int(sys.argv[3]) if len(sys.argv) > 3 else 0     # > 0: that many images via dbs.greedy_many
 cfg = hbx.rgb_config(1024)
 g = torch.Generator(device="cuda").manual_seed(0)
 pre = torch.rand((24, 1024, 1024), generator=g, device="cuda")
 tgt = torch.rand((3, 1024, 1024), generator=g, device="cuda")
 order = np.random.default_rng(3).permutation(24 * 1024 * 1024)[:n]
+if many:
+    plans = [hbx.Plan(cfg, max_jobs=3) for _ in range(many)]
+    gens = [torch.Generator(device="cuda").manual_seed(100 + i) for i in range(many)]
+    masks = [hbx.pack_bits(torch.rand((24, 1024, 1024), generator=g, device="cuda") >= 0.5) for g in gens]
+    tgts = [torch.rand((3, 1024, 1024), generator=g, device="cuda") for g in gens]
+    orders = [np.random.default_rng(3 + i).permutation(24 * 1024 * 1024)[:n] for i in range(many)]
+    dbs.greedy_many(plans, [m.clone() for m in masks], tgts, [o[:256] for o in orders])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = dbs.greedy_many(plans, masks, tgts, orders)
+    dt = time.perf_counter() - t0
+    tot = sum(r.steps for r in res)
+    print(f"greedy_many x{many}: {tot} candidates, {sum(len(r.accepted_positions) for r in res)} accepted, "
+          f"{dt:.3f} s, {tot / dt:.1f} candidates/s aggregate, {tot / dt / many:.1f} per image")
+    sys.exit(0)
 plan = hbx.Plan(cfg, max_jobs=256)
 m = hbx.pack_bits(pre >= 0.5)
 dbs.greedy(plan, m.clone(), tgt, order[:256], mode=mode)
