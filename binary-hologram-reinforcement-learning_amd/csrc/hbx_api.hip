@@ -781,8 +781,12 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   rc = ensure_hpsf(p, st);
   if (rc) return rc;
   const PlanDev& pd = p->pd;
-  const size_t need = (size_t)K * hbx::walk_blocks_per_job(pd.N, K) * 2;
-  if (need > p->walk_partial_elems) {   // allocation: first call per K range, outside capture
+  // sized once for every K, so the buffer never moves: launches captured into a
+  // graph (one per K) stay valid
+  size_t need = 0;
+  for (int k = 1; k <= hbx::kWalkMaxK; ++k)
+    need = std::max(need, (size_t)k * hbx::walk_blocks_per_job(pd.N, k) * 2);
+  if (need > p->walk_partial_elems) {   // allocation: first call only, outside capture
     if (p->walk_partial) (void)hipFree(p->walk_partial);
     p->walk_partial = nullptr;
     p->walk_partial_elems = 0;

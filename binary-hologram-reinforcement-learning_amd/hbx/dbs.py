@@ -94,9 +94,10 @@ class _Walk:
     turn (greedy_many): their latency-bound launches then overlap on the GPU."""
 
     def __init__(self, plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream,
-                 refresh_every, chunk: int = 64, progress=None):
+                 refresh_every, chunk: int = 64, progress=None, graphs: bool = False):
         self.plan, self.mask, self.target, self.order_t = plan, mask, target, order_t
         self.chunk, self.progress = chunk, progress
+        self.use_graphs, self.graphs = graphs, {}
         dev = plan.device
         self.s = s = stream if stream is not None else torch.cuda.current_stream()
         s.wait_stream(torch.cuda.current_stream())    # inputs written on the caller's stream
@@ -137,10 +138,28 @@ class _Walk:
         self.finished = False
         self.t0 = time.perf_counter()
 
+    def _chunk(self, stream):
+        self.plan.dbs_walk_psf(self.mask, self.target, self.base_stats, self.field, self.inten, self.order_t,
+                               self.wbuf, self.log_pos, self.log_psnr, self.k, self.chunk, stream=stream)
+
     def issue(self):
         slot = self.issued % 2
-        self.plan.dbs_walk_psf(self.mask, self.target, self.base_stats, self.field, self.inten, self.order_t,
-                               self.wbuf, self.log_pos, self.log_psnr, self.k, self.chunk, stream=self.s)
+        if not self.use_graphs:
+            self._chunk(self.s)
+        else:
+            # one captured chunk per speculation depth K (the walk buffers never move), replayed
+            g = self.graphs.get(self.k)
+            if g is None:
+                self._chunk(self.s)                        # this chunk runs eagerly
+                g = torch.cuda.CUDAGraph()
+                if not hasattr(self, "cap_stream"):
+                    self.cap_stream = torch.cuda.Stream(device=self.plan.device)   # capture needs a side stream
+                with torch.cuda.graph(g, stream=self.cap_stream):
+                    self._chunk(None)                      # recorded, not run; replayed on self.s
+                self.graphs[self.k] = g
+            else:
+                with torch.cuda.stream(self.s):
+                    g.replay()
         with torch.cuda.stream(self.s):
             self.pinned[slot].copy_(self.wbuf, non_blocking=True)
         self.events[slot].record(self.s)
@@ -220,10 +239,10 @@ class _Walk:
 
 
 def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream,
-                 refresh_every, chunk: int = 64, progress=None) -> GreedyResult:
+                 refresh_every, chunk: int = 64, progress=None, graphs: bool = False) -> GreedyResult:
     """greedy(mode="psf") on the device-resident walk (hbx_dbs_walk_psf)."""
     w = _Walk(plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream, refresh_every, chunk,
-              progress)
+              progress, graphs)
     while not w.finished:
         w.advance()
     return w.result()
@@ -262,7 +281,8 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
 
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
-           stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None) -> GreedyResult:
+           stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None,
+           graphs: bool = False) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
     mode="fft": every candidate is a full propagation of its colour group.
@@ -280,7 +300,7 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
         total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
         return _greedy_walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
-                            stream, refresh_every, progress=progress)
+                            stream, refresh_every, progress=progress, graphs=graphs)
     mode = "psf" if mode == "psf_host" else mode
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)

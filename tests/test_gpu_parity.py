@@ -706,6 +706,23 @@ def test_dbs_walk_early_stop_and_prefix():
     assert all(p < 777 for p in res.accepted_positions)
 
 
+def test_dbs_walk_graph_replay_matches(golden_dir):
+    """The walk's chunks captured into hipGraphs (one per speculation depth K)
+    and replayed give the eager walk's accept sequence: the C-ABI enqueues
+    capture-safe work (no allocation, copy or sync inside a launch)."""
+    import hbx
+    from hbx import dbs
+    d = load(golden_dir, "dbs_trace_64.npz")
+    plan = hbx.Plan(dev_cfg(small_rgb()), max_jobs=8)
+    res = []
+    for graphs in (False, True):
+        mask = hbx.pack_bits(torch.from_numpy(d["pre_model"]).cuda() >= 0.5)
+        res.append(dbs.greedy(plan, mask, torch.from_numpy(d["target"]).cuda(), d["order"], mode="psf",
+                              refresh_every=64, graphs=graphs))
+    assert res[0].accepted_positions == res[1].accepted_positions == np.nonzero(d["accepted"])[0].tolist()
+    assert res[0].final_psnr == res[1].final_psnr
+
+
 def test_dbs_greedy_many_equals_single_walks():
     """dbs.greedy_many (several images' walks side by side, one stream each)
     returns exactly what greedy(mode="psf") returns for each image alone,

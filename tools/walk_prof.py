@@ -38,10 +38,10 @@ if many:
     sys.exit(0)
 plan = hbx.Plan(cfg, max_jobs=256)
 m = hbx.pack_bits(pre >= 0.5)
-dbs.greedy(plan, m.clone(), tgt, order[:256], mode=mode)
+dbs.greedy(plan, m.clone(), tgt, order[:256], mode=mode, graphs=os.environ.get("HBX_WALK_GRAPHS") == "1")
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-r = dbs.greedy(plan, m, tgt, order, mode=mode)
+r = dbs.greedy(plan, m, tgt, order, mode=mode, graphs=os.environ.get("HBX_WALK_GRAPHS") == "1")
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 print(f"{mode}: {r.steps} candidates, {len(r.accepted_positions)} accepted, {r.launches} batches, "
