@@ -419,8 +419,8 @@ int hbx_propagate(hbx_plan_t p, const uint64_t* mask, const float* target, int32
                   float* intensity, double* chan_stats, double* psnr, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (!mask || !target || !chan_stats || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
-  if (n_env == 0) return HBX_OK;
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");  // empty: null buffers allowed
+  if (!mask || !target || !chan_stats) return fail(HBX_ERR_INVALID, "null buffer");
   HBX_HIP(hipSetDevice(p->device));
   return propagate_full(p, mask, target, nullptr, n_env, intensity, chan_stats, psnr, nullptr,
                         nullptr, (hipStream_t)stream);
@@ -430,8 +430,8 @@ int hbx_simulate(hbx_plan_t p, const uint64_t* mask, int32_t n_env, float* field
                  void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (!mask || !field || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
-  if (n_env == 0) return HBX_OK;
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  if (!mask || !field) return fail(HBX_ERR_INVALID, "null buffer");
   HBX_HIP(hipSetDevice(p->device));
   return propagate_full(p, mask, nullptr, nullptr, n_env, intensity, nullptr, nullptr, nullptr,
                         reinterpret_cast<float2*>(field), (hipStream_t)stream);
@@ -440,8 +440,8 @@ int hbx_simulate(hbx_plan_t p, const uint64_t* mask, int32_t n_env, float* field
 int hbx_psnr(hbx_plan_t p, const double* chan_stats, int32_t n_env, double* psnr, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (!chan_stats || !psnr || n_env < 0) return fail(HBX_ERR_INVALID, "null buffer / n_env");
-  if (n_env == 0) return HBX_OK;
+  if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  if (!chan_stats || !psnr) return fail(HBX_ERR_INVALID, "null buffer");
   HBX_HIP(hipSetDevice(p->device));
   HBX_HIP(hbx::launch_psnr(chan_stats, n_env, p->pd.G, psnr, pixel_count(p), p->optics.rel_scale,
                            p->optics.peak, (hipStream_t)stream));
@@ -597,9 +597,9 @@ int hbx_step(hbx_plan_t p, uint64_t* mask, const int64_t* actions, int32_t n_env
              int32_t accept_rule, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (!mask || !actions || !target || !chan_stats || !prev_psnr) return fail(HBX_ERR_INVALID, "null buffer");
   if (accept_rule != HBX_ACCEPT_ENV && accept_rule != HBX_ACCEPT_DBS) return fail(HBX_ERR_INVALID, "accept_rule");
   if (n_env <= 0) return n_env == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+  if (!mask || !actions || !target || !chan_stats || !prev_psnr) return fail(HBX_ERR_INVALID, "null buffer");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   const PlanDev& pd = p->pd;
@@ -624,9 +624,9 @@ int hbx_eval_flips(hbx_plan_t p, const uint64_t* base_mask, const float* target,
                    double* group_stats, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");  // empty batch: null buffers allowed
   if (!base_mask || !target || !base_chan_stats || !flips || !psnr_out)
     return fail(HBX_ERR_INVALID, "null buffer");
-  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   const PlanDev& pd = p->pd;
@@ -719,9 +719,9 @@ int hbx_eval_flips_psf(hbx_plan_t p, const uint64_t* base_mask, const float* tar
                        void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   if (!base_mask || !target || !base_chan_stats || !field || !intensity || !flips || !psnr_out)
     return fail(HBX_ERR_INVALID, "null buffer");
-  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   rc = ensure_hpsf(p, st);

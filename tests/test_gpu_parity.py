@@ -937,3 +937,40 @@ def test_crop_896_dbs_greedy_vs_oracle():
         if np.array_equal(got, acc):
             assert np.array_equal(m.cpu().numpy().view("<u8"), O.pack_mask(env.state)), mode
     plan.close()
+
+
+def test_empty_batches_and_chunked_invalid_flips():
+    """Edge cases at the C-ABI: zero-sized batches are no-ops (torch hands
+    null data pointers for empty tensors), a flip batch larger than max_jobs
+    runs in max_jobs chunks, and out-of-range flip indices (negative, or
+    >= CH*N^2, which env.py:157-161's decode would carry into a non-existent
+    plane) come back as NaN without disturbing their neighbours."""
+    import hbx
+    ocfg = small_rgb()
+    pre, tgt = O.synthetic_inputs(ocfg, 5)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=3)
+    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
+    t = torch.from_numpy(tgt).cuda()
+
+    inten, st0, ps0 = plan.propagate(bits[None][:0], t[None][:0])
+    assert inten.shape[0] == 0 and st0.shape[0] == 0 and ps0.shape[0] == 0
+    assert plan.psnr(st0).shape == (0,)
+
+    _, st, ps = plan.propagate(bits[None], t[None])
+    got0, gs0 = plan.eval_flips(bits, t, st[0].contiguous(), torch.empty((0,), dtype=torch.int64, device="cuda"))
+    assert got0.shape == (0,) and gs0.shape == (0, 3)
+
+    env = O.OracleEnv(ocfg)
+    env.reset(pre, tgt)
+    assert abs(float(ps[0]) - env.initial_psnr) <= PSNR_TOL
+    total = ocfg.channels * 64 * 64
+    flips = np.array([0, -1, total - 1, total, 4095, 4096, 2 * 4096 + 65], np.int64)   # K = 7 > max_jobs
+    got, _ = plan.eval_flips(bits, t, st[0].contiguous(), torch.from_numpy(flips).cuda())
+    got = got.cpu().numpy()
+    for a, g in zip(flips, got):
+        if 0 <= a < total:
+            assert abs(g - env.evaluate_flip(int(a))[0]) <= PSNR_TOL, int(a)
+        else:
+            assert np.isnan(g), int(a)
+    # the base mask is untouched by evaluation
+    assert np.array_equal(bits.cpu().numpy(), to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8))).cpu().numpy())
