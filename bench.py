@@ -277,7 +277,12 @@ def main():
     from hbx.env import HologramVecEnv
     from hbx.plan import mono_config, rgb_config
 
-    rank, world, local = hd.init()
+    # HBX_BENCH_REHEARSE_ONE_GPU=1: every rank on cuda:0 over gloo -- rehearses the world > 1
+    # code path on a one-GPU box (RCCL refuses two ranks on one device); never a measurement
+    rehearse = os.environ.get("HBX_BENCH_REHEARSE_ONE_GPU") == "1"
+    rank, world, local = hd.init(backend="gloo" if rehearse else None)
+    if rehearse:
+        local = 0
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local)
