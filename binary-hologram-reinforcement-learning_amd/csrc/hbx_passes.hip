@@ -274,6 +274,8 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #pragma unroll
     for (int k2 = 0; k2 < R; ++k2) hall[k2] = buf_ld2(rh, vh, k2 * R * 8);
 #define COL2_H(k2) hall[k2]
+#elif defined(HBX_COL2_NOH)   // timing experiment only: no H loads (numerically meaningless)
+#define COL2_H(k2) make_float2(1.0f, 0.0f)
 #else
 #define COL2_H(k2) buf_ld2(rh, vh, (k2) * R * 8)
 #endif
