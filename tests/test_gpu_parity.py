@@ -974,3 +974,33 @@ def test_empty_batches_and_chunked_invalid_flips():
             assert np.isnan(g), int(a)
     # the base mask is untouched by evaluation
     assert np.array_equal(bits.cpu().numpy(), to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8))).cpu().numpy())
+
+
+@pytest.mark.timeout(240)
+def test_sharded_envs_world2_match_single_process():
+    """SURVEY 8e on the device: 4 envs split 2 + 2 over a world of 2 (gloo,
+    both ranks on cuda:0 -- the one-GPU stand-in for one rank per GPU over
+    RCCL), each rank stepping its own envs and gathering every step's metrics
+    to rank 0, reproduce a single process stepping all 4 envs bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    from tests import _shard_worker as W
+
+    want = np.stack([r.cpu().numpy() for r in W.run_envs(0, W.TOTAL)])
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=W.worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    got = next(r for r in res if r is not None)
+    assert got.shape == want.shape == (W.STEPS, W.TOTAL, 5)
+    assert np.array_equal(got, want)
+    assert 0 < want[:, :, 2].sum() < want[:, :, 2].size   # both accepts and rollbacks occurred
