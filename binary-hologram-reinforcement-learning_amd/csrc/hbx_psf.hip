@@ -94,8 +94,27 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
     const float4* I = reinterpret_cast<const float4*>(inten + ((size_t)jb.env * G + g) * hw);
     const float4* T = reinterpret_cast<const float4*>(target + ((size_t)jb.env * G + g) * hw);
     const float2* h = hpsf + (size_t)g * hw;
-    const int nq = (int)(hw / 4);
-    for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
+#ifndef HBX_PSF_QUAD   // one pixel per lane: the shifted h reads coalesce per wave (measured 0.457 -> 0.445 and 0.427 -> 0.419 ms
+                       // per 128-job launch vs four pixels per lane, `make exp EXP=PSF_QUAD`; tools/psf_ab.sh)
+    const float2* U2 = field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw;
+    const float* I1 = inten + ((size_t)jb.env * G + g) * hw;
+    const float* T1 = target + ((size_t)jb.env * G + g) * hw;
+    const int npx = (int)hw;
+#pragma unroll 4
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < npx; q += kPsfBlocks * 256) {
+      const int y = q / N, x = q % N;
+      const float2 u = U2[q];
+      const float iv = I1[q], tv = T1[q];
+      const float2 hv = h[(size_t)fold(y - r, N) * N + fold(x - col, N)];
+      const float nr = fmaf(delta, hv.x, u.x), ni = fmaf(delta, hv.y, u.y);
+      const float d = fmaf(nr, nr, ni * ni) - fmaf(u.x, u.x, u.y * u.y);
+      const float In = fmaf(d, invp, iv);
+      sxy = fma((double)In, (double)tv, sxy);
+      sxx = fma((double)In, (double)In, sxx);
+    }
+    if (false)
+#endif
+    for (int q = blockIdx.x * 256 + threadIdx.x; q < (int)(hw / 4); q += kPsfBlocks * 256) {
       const int y = (4 * q) / N, x0 = (4 * q) % N;
       const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
       const float4 iv = I[q], tv = T[q];
