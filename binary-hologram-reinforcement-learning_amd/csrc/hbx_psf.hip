@@ -70,7 +70,7 @@ __global__ void k_psf_order(const JobDesc* __restrict__ jobs, int n_jobs, int G,
   }
 }
 
-// grid (kPsfBlocks, n_jobs); each thread walks quads of 4 consecutive pixels
+// grid (kPsfBlocks, n_jobs); each thread walks single pixels (HBX_PSF_QUAD: quads of 4 consecutive pixels)
 __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jobs,
                                                   const int32_t* __restrict__ order,
                                                   const uint64_t* __restrict__ mask,
