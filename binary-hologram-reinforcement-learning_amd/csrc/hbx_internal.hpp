@@ -124,7 +124,10 @@ struct PlanDev {
   PassTimer* timer;    // nullable
 };
 
-constexpr int kPsfBlocks = 64;   // blocks per job of the incremental-field kernels
+#ifndef HBX_PSF_BLOCKS   // A/B switch: `make exp EXP=PSF_BLOCKS=128`
+#define HBX_PSF_BLOCKS 128   // measured 128 > 256 > 64 > 32 (profiles/r01_psf_blocks_ab.txt)
+#endif
+constexpr int kPsfBlocks = HBX_PSF_BLOCKS;   // blocks per job of the incremental-field kernels
 
 // N = 1024 class tables appended to PlanDev::tw (hbx_colbits.hip): class c = 0..32 at
 // kTwClassOff + c * kTwClassStride: [8][16] nibble tables sum_j v_j W32^{(c mod 32)(4k + j)},
