@@ -267,6 +267,23 @@ int hbx_plan_destroy(hbx_plan_t p) {
 
 size_t hbx_plan_workspace_bytes(hbx_plan_t p) { return p ? p->ws_bytes : 0; }
 
+int hbx_plan_set_precision(hbx_plan_t p, int32_t precision) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (precision < HBX_PRECISION_F32 || precision > HBX_PRECISION_F16_STORE)
+    return fail(HBX_ERR_INVALID, "precision must be HBX_PRECISION_F32, _BF16_STORE or _F16_STORE");
+  if (precision != HBX_PRECISION_F32 && (p->pd.R == 0 || p->pd.colbits))
+    return fail(HBX_ERR_UNSUPPORTED, "reduced-precision intermediates: N = 64 / 256 / 1024 three-pass path only");
+  p->pd.store_kind = precision;
+  return HBX_OK;
+}
+
+int hbx_plan_precision(hbx_plan_t p) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  return p->pd.store_kind;
+}
+
 int hbx_plan_pipeline(hbx_plan_t p) {
   int rc = check_plan(p);
   if (rc) return rc;
@@ -701,15 +718,16 @@ int hbx_flip_map(hbx_plan_t p, const uint64_t* mask, const float* target, float*
 
 int hbx_commit_flip(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, double* prev_psnr,
                     const int64_t* flips, const double* psnr_out, const double* group_stats,
-                    const int32_t* k, void* stream) {
+                    const int32_t* k, int32_t K, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   if (!base_mask || !base_chan_stats || !prev_psnr || !flips || !psnr_out || !group_stats || !k)
     return fail(HBX_ERR_INVALID, "null buffer");
   HBX_HIP(hipSetDevice(p->device));
   const PlanDev& pd = p->pd;
   HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
-                                  0x7fffffff, pd.G, pd.P, pd.N, pd.N, (hipStream_t)stream));
+                                  K, pd.G, pd.P, pd.N, pd.N, (hipStream_t)stream));
   return HBX_OK;
 }
 
@@ -742,9 +760,10 @@ int hbx_eval_flips_psf(hbx_plan_t p, const uint64_t* base_mask, const float* tar
 
 int hbx_commit_flip_psf(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, double* prev_psnr,
                         float* field, float* intensity, const int64_t* flips, const double* psnr_out,
-                        const double* group_stats, const int32_t* k, void* stream) {
+                        const double* group_stats, const int32_t* k, int32_t K, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   if (!base_mask || !base_chan_stats || !prev_psnr || !field || !intensity || !flips || !psnr_out ||
       !group_stats || !k)
     return fail(HBX_ERR_INVALID, "null buffer");
@@ -756,8 +775,8 @@ int hbx_commit_flip_psf(hbx_plan_t p, uint64_t* base_mask, double* base_chan_sta
   const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
   // toggle the mask bit first: the field update's delta is read from the new bit
   HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
-                                  0x7fffffff, G, P, N, N, st));
-  HBX_HIP(hbx::launch_job_from_flip_k(flips, k, N, N, P, CH, p->jobs, pd.psf_order, p->accept_flag, st));
+                                  K, G, P, N, N, st));
+  HBX_HIP(hbx::launch_job_from_flip_k(flips, k, K, N, N, P, CH, p->jobs, pd.psf_order, p->accept_flag, st));
   // psf_order is already {0}: launch_psf_commit visits the single job
   HBX_HIP(hbx::launch_psf_commit(pd, p->jobs, 1, base_mask, reinterpret_cast<float2*>(field), intensity,
                                  p->accept_flag, st));
@@ -765,7 +784,8 @@ int hbx_commit_flip_psf(hbx_plan_t p, uint64_t* base_mask, double* base_chan_sta
 }
 
 int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, double* base_chan_stats,
-                     float* field, float* intensity, const int64_t* order, hbx_dbs_walk_t* walk,
+                     float* field, float* intensity, const int64_t* order, int64_t n_order,
+                     hbx_dbs_walk_t* walk,
                      int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int32_t K,
                      int32_t batches, void* stream) {
   int rc = check_plan(p);
@@ -776,6 +796,7 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
     return fail(HBX_ERR_INVALID, "accept log");
   if (K < 1 || K > hbx::kWalkMaxK) return fail(HBX_ERR_INVALID, "K must be in [1, 256]");
   if (batches < 0) return fail(HBX_ERR_INVALID, "batches");
+  if (n_order < 0) return fail(HBX_ERR_INVALID, "n_order");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   rc = ensure_hpsf(p, st);
@@ -801,6 +822,7 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   l.field = reinterpret_cast<float2*>(field);
   l.inten = intensity;
   l.order = order;
+  l.n_order = n_order;
   l.walk = walk;
   l.log_pos = accept_pos;
   l.log_psnr = accept_psnr;
@@ -836,11 +858,30 @@ int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
   if (capacity == 0) return HBX_OK;
   tm = new (std::nothrow) hbx::PassTimer();
   if (!tm) return fail(HBX_ERR_NOMEM, "timer");
+  // on any failure below, destroy exactly the events created so far
+  auto undo = [tm](int passes_done, int events_in_pass) {
+    for (int k = 0; k <= passes_done && k < hbx::kNumPasses; ++k) {
+      if (!tm->ev[k]) continue;
+      const int n = k < passes_done ? 2 * tm->capacity : events_in_pass;
+      for (int i = 0; i < n; ++i) (void)hipEventDestroy(tm->ev[k][i]);
+      delete[] tm->ev[k];
+    }
+    delete tm;
+  };
   tm->capacity = capacity;
   for (int k = 0; k < hbx::kNumPasses; ++k) {
     tm->ev[k] = new (std::nothrow) hipEvent_t[2 * (size_t)capacity];
-    if (!tm->ev[k]) return fail(HBX_ERR_NOMEM, "timer events");
-    for (int i = 0; i < 2 * capacity; ++i) HBX_HIP(hipEventCreate(&tm->ev[k][i]));
+    if (!tm->ev[k]) {
+      undo(k, 0);
+      return fail(HBX_ERR_NOMEM, "timer events");
+    }
+    for (int i = 0; i < 2 * capacity; ++i) {
+      const hipError_t e = hipEventCreate(&tm->ev[k][i]);
+      if (e != hipSuccess) {
+        undo(k, i);
+        return fail(HBX_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e));
+      }
+    }
   }
   p->pd.timer = tm;
   return HBX_OK;

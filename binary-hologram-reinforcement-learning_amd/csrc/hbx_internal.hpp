@@ -20,6 +20,18 @@ __device__ __forceinline__ double psnr_from(double sxy, double sxx, double syy, 
   return 10.0 * log10(peak * peak / mse);
 }
 
+// Increment of one pixel's plane-mean intensity when a flip adds delta * h to
+// its field u: (|u + delta h|^2 - |u|^2) / P = delta (2 Re(u conj h) + delta |h|^2) / P,
+// formed without the two squares, so its f32 error is relative to the
+// increment itself (differencing the squares loses it to the rounding of |u|^2
+// wherever |h| << |u|, i.e. almost everywhere: ~1e-10 dB of noise per 1024x24
+// candidate).  Incremental-field kernels (hbx_psf.hip, hbx_walk.hip).
+__device__ __forceinline__ float flip_dI(float ur, float ui, float hr, float hi, float delta, float invp) {
+  const float re = fmaf(ur, hr, ui * hi);
+  const float hh = fmaf(hr, hr, hi * hi);
+  return delta * fmaf(delta, hh, 2.0f * re) * invp;
+}
+
 // One colour-group propagation: env index (plan-local), group, optional flip.
 struct JobDesc {
   int32_t env;         // < 0: invalid job (skipped, outputs neutral)
@@ -120,6 +132,7 @@ struct PlanDev {
   int32_t* psf_order;  // [max_jobs] jobs sorted by colour group (launch order)
   float* zero_row;     // [N] zeros: the target row of a propagation without a target
   int colbits;         // N = 1024: bits -> column pass without the A intermediate (hbx_colbits.hip)
+  int store_kind;      // HBX_PRECISION_*: rounding of the pass intermediates (0 = f32, the product)
   int fused896;        // N = 896: fused three-pass path (hbx_passes896.hip); 0 = composed (hbx_generic.hip)
   PassTimer* timer;    // nullable
 };
@@ -197,6 +210,7 @@ struct WalkLaunch {
   float2* field;
   float* inten;
   const int64_t* order;
+  int64_t n_order;   // length of order: the walk never visits past min(walk->total, n_order)
   hbx_dbs_walk_t* walk;
   int64_t* log_pos;
   double* log_psnr;
@@ -215,7 +229,7 @@ hipError_t launch_jobs_from_actions(const int64_t* actions, int n, int H, int W,
                                     JobDesc* jobs, int32_t* err, hipStream_t st);
 hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int P, int CH,
                                   JobDesc* jobs, hipStream_t st);
-hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int H, int W, int P, int CH,
+hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int K, int H, int W, int P, int CH,
                                   JobDesc* jobs, int32_t* order, int32_t* accept, hipStream_t st);
 hipError_t launch_jobs_full(const int32_t* env_ids, int n_ids, int G, JobDesc* jobs, hipStream_t st);
 hipError_t launch_full_finalize(const JobDesc* jobs, const double* job_stats, int n_ids, int G,

@@ -55,10 +55,11 @@ __global__ void k_jobs_from_flips(const int64_t* __restrict__ flips, int K, int 
 }
 
 // the one job of candidate flips[*k] (commit of a speculative batch)
-__global__ void k_job_from_flip_k(const int64_t* __restrict__ flips, const int32_t* __restrict__ k,
+__global__ void k_job_from_flip_k(const int64_t* __restrict__ flips, const int32_t* __restrict__ k, int K,
                                   int H, int W, int P, int CH, JobDesc* __restrict__ jobs,
                                   int32_t* __restrict__ order, int32_t* __restrict__ accept) {
-  const int64_t a = flips[*k];
+  const int kk = *k;
+  const int64_t a = (kk >= 0 && kk < K) ? flips[kk] : -1;   // k outside [0, K): nothing to commit
   const int64_t hw = (int64_t)H * W;
   JobDesc jd;
   if (a < 0 || a >= (int64_t)CH * hw) {
@@ -69,7 +70,7 @@ __global__ void k_job_from_flip_k(const int64_t* __restrict__ flips, const int32
   }
   jobs[0] = jd;
   order[0] = 0;
-  accept[0] = 1;
+  accept[0] = jd.env >= 0 ? 1 : 0;
 }
 
 // full-propagation jobs: (env_ids[i], g) for all groups
@@ -374,9 +375,9 @@ hipError_t launch_jobs_from_flips(const int64_t* flips, int K, int H, int W, int
                      CH, jobs);
   return hipGetLastError();
 }
-hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int H, int W, int P, int CH,
+hipError_t launch_job_from_flip_k(const int64_t* flips, const int32_t* k, int K, int H, int W, int P, int CH,
                                   JobDesc* jobs, int32_t* order, int32_t* accept, hipStream_t st) {
-  hipLaunchKernelGGL(k_job_from_flip_k, dim3(1), dim3(1), 0, st, flips, k, H, W, P, CH, jobs, order, accept);
+  hipLaunchKernelGGL(k_job_from_flip_k, dim3(1), dim3(1), 0, st, flips, k, K, H, W, P, CH, jobs, order, accept);
   return hipGetLastError();
 }
 hipError_t launch_jobs_full(const int32_t* env_ids, int n_ids, int G, JobDesc* jobs, hipStream_t st) {

@@ -32,23 +32,24 @@
 
 namespace hbx {
 
-// Precision study (SURVEY 8d cfg 5): `make exp EXP=BF16_STORE` / `EXP=F16_STORE` round every
-// value written to the two pass intermediates (row spectrum, column-pass output) to bf16 /
-// fp16, i.e. the numerics of half-width intermediate storage (the layout stays f32).  Never
-// part of the product build.
+// Precision study (SURVEY 8d cfg 5, hbx_plan_set_precision): SK = HBX_PRECISION_BF16_STORE /
+// _F16_STORE rounds every value written to the two pass intermediates (row spectrum,
+// column-pass output) to bf16 / fp16, i.e. the numerics of half-width intermediate storage
+// (the layout stays f32).  SK = HBX_PRECISION_F32 is the product path (no rounding code).
+template <int SK>
 __device__ __forceinline__ float2 store_round(float2 v) {
-#if defined(HBX_BF16_STORE)
-  auto r = [](float x) {
-    uint32_t u = __float_as_uint(x);
-    u += 0x7fffu + ((u >> 16) & 1u);   // round to nearest even
-    return __uint_as_float(u & 0xffff0000u);
-  };
-  return make_float2(r(v.x), r(v.y));
-#elif defined(HBX_F16_STORE)
-  return make_float2((float)(_Float16)v.x, (float)(_Float16)v.y);
-#else
-  return v;
-#endif
+  if constexpr (SK == HBX_PRECISION_BF16_STORE) {
+    auto r = [](float x) {
+      uint32_t u = __float_as_uint(x);
+      u += 0x7fffu + ((u >> 16) & 1u);   // round to nearest even
+      return __uint_as_float(u & 0xffff0000u);
+    };
+    return make_float2(r(v.x), r(v.y));
+  } else if constexpr (SK == HBX_PRECISION_F16_STORE) {
+    return make_float2((float)(_Float16)v.x, (float)(_Float16)v.y);
+  } else {
+    return v;
+  }
 }
 
 // Threads per block of the row passes at N = 1024 (row_nt, hbx_internal.hpp).
@@ -76,7 +77,7 @@ using LayoutB = PanelLine<R, R * R, pan_b(R)>;
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
-template <int R, int NT>
+template <int R, int NT, int SK>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
                                                    const uint32_t* __restrict__ mask,
                                                    float2* __restrict__ ws_a,
@@ -172,8 +173,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
     const int c = threadIdx.x + NT * i;
     const int r2 = (c % (GPB / 2)) * 2;
     const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
-    const float2 a = store_round(tile[tile_pos<R, GPB>(line, r2)]);
-    const float2 b = store_round(tile[tile_pos<R, GPB>(line, r2 + 1)]);
+    const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
+    const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
     const int pl = line / (N / 2);
     // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
     st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
 
-template <int R>
+template <int R, int SK>
 __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
                                                  const float2* __restrict__ ws_a,
                                                  float2* __restrict__ ws_b,
@@ -327,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     {
       const int vo = PB::voff(t, kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
     }
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
       const int vo = PA::voff(t, kx + KSTEP);
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     {
       const int vo = PB::voff(t, dc ? N / 2 : N - kx);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
+      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
     }
   }
 #undef COL2_H
@@ -604,7 +605,7 @@ hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool
 __global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,
                                   double* __restrict__ job_stats);
 
-template <int R>
+template <int R, int SK>
 static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jobs,
                                 const uint32_t* mask, const float* target, float* inten_out,
                                 float2* field_out, hipStream_t st) {
@@ -620,7 +621,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R));
     if (tm) tm->begin(0, st);
-    hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
+    hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);
     if (tm) tm->end(0, n_jobs, st);
   }
@@ -628,7 +629,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if (tm) tm->begin(1, st);
     constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
     const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
-    hipLaunchKernelGGL(k_col2<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
+    hipLaunchKernelGGL((k_col2<R, SK>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
     if (tm) tm->end(1, n_jobs, st);
   }
   }
@@ -651,10 +652,19 @@ hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const ui
   if (pd.R == 0)
     return run_jobs_generic(pd, jobs, n_jobs, reinterpret_cast<const uint64_t*>(mask), target, inten_out,
                             field_out, st);
-  switch (pd.R) {
-    case 32: return launch_passes<32>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
-    case 16: return launch_passes<16>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
-    case 8: return launch_passes<8>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
+  switch (pd.R * 4 + pd.store_kind) {
+#define HBX_PASSES_CASE(R_, SK_) \
+    case R_ * 4 + SK_: return launch_passes<R_, SK_>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
+    HBX_PASSES_CASE(32, HBX_PRECISION_F32)
+    HBX_PASSES_CASE(32, HBX_PRECISION_BF16_STORE)
+    HBX_PASSES_CASE(32, HBX_PRECISION_F16_STORE)
+    HBX_PASSES_CASE(16, HBX_PRECISION_F32)
+    HBX_PASSES_CASE(16, HBX_PRECISION_BF16_STORE)
+    HBX_PASSES_CASE(16, HBX_PRECISION_F16_STORE)
+    HBX_PASSES_CASE(8, HBX_PRECISION_F32)
+    HBX_PASSES_CASE(8, HBX_PRECISION_BF16_STORE)
+    HBX_PASSES_CASE(8, HBX_PRECISION_F16_STORE)
+#undef HBX_PASSES_CASE
     default: return hipErrorInvalidValue;
   }
 }

@@ -8,7 +8,10 @@
 // the exact FFT path) and delta = vb * (1 - 2 bit_old) the change of the
 // field value (amplitude: +-1, phase: -+2).  A step therefore streams U_c
 // (8 B/px), I_g (4 B/px) and the target channel (4 B/px) once -- no FFT --
-// and the relative-PSNR sums come out of the same pass.  h_g is even in x
+// and the relative-PSNR sums come out of the same pass as the flip's
+// INCREMENTS sum dI T and sum (2 I + dI) dI (f64), added to the cached f64
+// channel sums: the decision then carries the increment's own f32 precision
+// (~1e-13 dB at 1024 x 24) instead of the rounding of a full-image sum.  h_g is even in x
 // and y (H_g depends on fx^2 and fy^2), so only its quadrant [0, N/2]^2 is
 // read (folded offsets): 2.1 MB per group at N = 1024, which stays in an
 // XCD's 4-MB L2 when the launch visits the jobs grouped by colour group
@@ -106,11 +109,9 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
       const float2 u = U2[q];
       const float iv = I1[q], tv = T1[q];
       const float2 hv = h[(size_t)fold(y - r, N) * N + fold(x - col, N)];
-      const float nr = fmaf(delta, hv.x, u.x), ni = fmaf(delta, hv.y, u.y);
-      const float d = fmaf(nr, nr, ni * ni) - fmaf(u.x, u.x, u.y * u.y);
-      const float In = fmaf(d, invp, iv);
-      sxy = fma((double)In, (double)tv, sxy);
-      sxx = fma((double)In, (double)In, sxx);
+      const float dI = flip_dI(u.x, u.y, hv.x, hv.y, delta, invp);
+      sxy = fma((double)dI, (double)tv, sxy);
+      sxx = fma((double)fmaf(2.0f, iv, dI), (double)dI, sxx);
     }
     if (false)
 #endif
@@ -127,12 +128,9 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
       const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float ur = uu[2 * k], ui = uu[2 * k + 1];
-        const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
-        const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
-        const float In = fmaf(d, invp, ii[k]);
-        sxy = fma((double)In, (double)tt[k], sxy);
-        sxx = fma((double)In, (double)In, sxx);
+        const float dI = flip_dI(uu[2 * k], uu[2 * k + 1], hh[2 * k], hh[2 * k + 1], delta, invp);
+        sxy = fma((double)dI, (double)tt[k], sxy);
+        sxx = fma((double)fmaf(2.0f, ii[k], dI), (double)dI, sxx);
       }
     }
   }
@@ -143,8 +141,9 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
   }
 }
 
-// fixed-order reduction of the block partials; sum T^2 of the touched channel
-// is unchanged by a flip and comes from the cached channel statistics
+// fixed-order reduction of the block partials (the flip's increments of sum IT
+// and sum I^2) added to the cached channel statistics; sum T^2 of the touched
+// channel is unchanged by a flip
 __global__ void k_psf_reduce(const JobDesc* __restrict__ jobs, const double* __restrict__ partial,
                              int n_jobs, int G, const double* __restrict__ chan_stats,
                              double* __restrict__ job_stats) {
@@ -154,9 +153,15 @@ __global__ void k_psf_reduce(const JobDesc* __restrict__ jobs, const double* __r
   double a = 0.0, b = 0.0;
   const double* p = partial + (size_t)j * kPsfBlocks * 2;
   for (int i = 0; i < kPsfBlocks; ++i) { a += p[2 * i]; b += p[2 * i + 1]; }
-  job_stats[3 * j] = a;
-  job_stats[3 * j + 1] = b;
-  job_stats[3 * j + 2] = jb.env >= 0 ? chan_stats[((size_t)jb.env * G + jb.group) * 3 + 2] : 0.0;
+  if (jb.env < 0) {
+    job_stats[3 * j] = job_stats[3 * j + 1] = job_stats[3 * j + 2] = 0.0;
+    return;
+  }
+  // the partials are the flip's increments; the flipped group's sums are base + increment
+  const double* base = chan_stats + ((size_t)jb.env * G + jb.group) * 3;
+  job_stats[3 * j] = base[0] + a;
+  job_stats[3 * j + 1] = base[1] + b;
+  job_stats[3 * j + 2] = base[2];
 }
 
 // accepted envs: rewrite U_c and I_g (the mask bit is already flipped)
@@ -194,11 +199,9 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float ur = uu[2 * k], ui = uu[2 * k + 1];
-      const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
-      const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
-      ii[k] = fmaf(d, invp, ii[k]);
-      uu[2 * k] = nr;
-      uu[2 * k + 1] = ni;
+      ii[k] += flip_dI(ur, ui, hh[2 * k], hh[2 * k + 1], delta, invp);
+      uu[2 * k] = fmaf(delta, hh[2 * k], ur);
+      uu[2 * k + 1] = fmaf(delta, hh[2 * k + 1], ui);
     }
     U[2 * q] = make_float4(uu[0], uu[1], uu[2], uu[3]);
     U[2 * q + 1] = make_float4(uu[4], uu[5], uu[6], uu[7]);

@@ -11,7 +11,8 @@
 //
 //   k_walk_eval    grid (bpj, K): block (x, j) streams slice x of candidate
 //                  j's plane field / group intensity / target (as k_psf_eval)
-//                  and writes its (sum I'T, sum I'^2) partial.
+//                  and writes its partial of the flip's increments
+//                  (sum dI T, sum (2 I + dI) dI; f64).
 //   k_walk_decide  one block: reduces every candidate's partials in fixed
 //                  order, forms the PSNRs, picks the first improving candidate
 //                  in visiting order and applies it: mask bit, group
@@ -71,7 +72,8 @@ struct WalkArgs {
   double* base_stats;        // [G][3]
   float2* field;             // [CH][N][N]
   float* inten;              // [G][N][N]
-  const int64_t* order;      // [total]
+  const int64_t* order;      // [n_order]
+  int64_t n_order;
   hbx_dbs_walk_t* w;
   int64_t* log_pos;
   double* log_psnr;
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_eval(WalkArgs a) {
   hbx_dbs_walk_t* w = a.w;
   // uniform control state: written only by earlier launches' last blocks
   if (w->done || w->halt) return;
-  const int64_t pos = w->pos, total = w->total;
+  const int64_t pos = w->pos, total = w->total < a.n_order ? w->total : a.n_order;
   const int N = a.N, P = a.P, CH = a.G * a.P;
   const size_t hw = (size_t)N * N;
   const int j = blockIdx.y;
@@ -121,12 +123,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_eval(WalkArgs a) {
         const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float ur = uu[2 * k], ui = uu[2 * k + 1];
-          const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
-          const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
-          const float In = fmaf(d, invp, ii[k]);
-          sxy = fma((double)In, (double)tt[k], sxy);
-          sxx = fma((double)In, (double)In, sxx);
+          const float dI = flip_dI(uu[2 * k], uu[2 * k + 1], hh[2 * k], hh[2 * k + 1], delta, invp);
+          sxy = fma((double)dI, (double)tt[k], sxy);
+          sxx = fma((double)fmaf(2.0f, ii[k], dI), (double)dI, sxx);
         }
       }
     }
@@ -153,10 +152,11 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
     if (threadIdx.x == 0) w->commit_ch = -1;
     return;
   }
-  const int64_t pos = ws.pos, total = ws.total;
+  const int64_t pos = ws.pos, total = ws.total < a.n_order ? ws.total : a.n_order;
   const int N = a.N, P = a.P, CH = a.G * a.P, G = a.G;
   const size_t hw = (size_t)N * N;
-  const int kv = (int)((total - pos) < (int64_t)a.K ? (total - pos) : (int64_t)a.K);
+  const int64_t left = total > pos ? total - pos : 0;
+  const int kv = (int)(left < (int64_t)a.K ? left : (int64_t)a.K);
   const int bpj = a.bpj;
   // the candidates' actions and the base statistics, in flight with the partials
   int64_t act = -1;
@@ -204,6 +204,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
     double ps = NAN;
     if (act >= 0 && act < (int64_t)CH * (int64_t)hw) {
       const int g = (int)(act / (int64_t)hw) / P;
+      // the partials are the flip's increments: candidate group sums = base + increment
+      s_sxy[cc] += bs[3 * g];
+      s_sxx[cc] += bs[3 * g + 1];
       double sxy2 = 0.0, sxx2 = 0.0, syy2 = 0.0;
 #pragma unroll
       for (int gg = 0; gg < HBX_MAX_GROUPS; ++gg) {
@@ -284,11 +287,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_commit(WalkArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float ur = uu[2 * k], ui = uu[2 * k + 1];
-      const float nr = fmaf(delta, hh[2 * k], ur), ni = fmaf(delta, hh[2 * k + 1], ui);
-      const float d = fmaf(nr, nr, ni * ni) - fmaf(ur, ur, ui * ui);
-      ii[k] = fmaf(d, invp, ii[k]);
-      uu[2 * k] = nr;
-      uu[2 * k + 1] = ni;
+      ii[k] += flip_dI(ur, ui, hh[2 * k], hh[2 * k + 1], delta, invp);
+      uu[2 * k] = fmaf(delta, hh[2 * k], ur);
+      uu[2 * k + 1] = fmaf(delta, hh[2 * k + 1], ui);
     }
     U[2 * q] = make_float4(uu[0], uu[1], uu[2], uu[3]);
     U[2 * q + 1] = make_float4(uu[4], uu[5], uu[6], uu[7]);
@@ -314,6 +315,7 @@ hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
   a.field = l.field;
   a.inten = l.inten;
   a.order = l.order;
+  a.n_order = l.n_order;
   a.w = l.walk;
   a.log_pos = l.log_pos;
   a.log_psnr = l.log_psnr;

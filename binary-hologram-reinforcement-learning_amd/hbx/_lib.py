@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 5
+ABI_VERSION = 6
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -23,6 +23,7 @@ ACCEPT_ENV, ACCEPT_DBS = 0, 1
 REWARD_PSNR, REWARD_IMPORTANCE = 0, 1
 MAX_GROUPS = 4
 WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
+PRECISION_F32, PRECISION_BF16_STORE, PRECISION_F16_STORE = 0, 1, 2   # hbx_plan_set_precision
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
@@ -30,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
+    "hbx_plan_set_precision", "hbx_plan_precision",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -108,15 +110,17 @@ def _declare(lib):
                                  VP, VP, VP, VP, VP]
     lib.hbx_step.argtypes = [VP, VP, VP, I32, VP, VP, VP, VP, VP, I32, VP]
     lib.hbx_eval_flips.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP]
-    lib.hbx_commit_flip.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP]
+    lib.hbx_commit_flip.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]
     lib.hbx_env_step_psf.argtypes = [VP, C.POINTER(EnvBuffers), C.POINTER(EnvParams), I32, VP, VP, VP,
                                      VP, VP, VP, VP]
     lib.hbx_field_refresh.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, VP]
     lib.hbx_simulate.argtypes = [VP, VP, I32, VP, VP, VP]
     lib.hbx_flip_map.argtypes = [VP, VP, VP, VP, VP, VP]
     lib.hbx_eval_flips_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, I32, VP, VP, VP]
-    lib.hbx_commit_flip_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, VP]
-    lib.hbx_dbs_walk_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, C.c_int64, I32, I32, VP]
+    lib.hbx_commit_flip_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, VP, VP, VP, I32, VP]
+    lib.hbx_dbs_walk_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, I64, VP, VP, VP, I64, I32, I32, VP]
+    lib.hbx_plan_set_precision.argtypes = [VP, I32]
+    lib.hbx_plan_precision.argtypes = [VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]

@@ -261,8 +261,12 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
     exactly greedy(mode="psf") on that image alone; masks are modified in place."""
     if not (len(plans) == len(masks) == len(targets) == len(orders)):
         raise ValueError("one plan, mask, target and order per image")
-    results: List[GreedyResult] = []
     step = max(1, int(concurrency))
+    for g0 in range(0, len(plans), step):
+        # each walk writes its plan's walk partials and job workspace from its own stream
+        if len({id(p) for p in plans[g0:g0 + step]}) < len(plans[g0:g0 + step]):
+            raise ValueError("greedy_many: walks running side by side need distinct Plan objects")
+    results: List[GreedyResult] = []
     for g0 in range(0, len(plans), step):
         walks = []
         for plan, mask, target, order in zip(plans[g0:g0 + step], masks[g0:g0 + step], targets[g0:g0 + step],

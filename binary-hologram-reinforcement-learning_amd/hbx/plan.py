@@ -135,7 +135,8 @@ class Plan:
     """hbx_plan_t owner.  ``max_jobs`` bounds the group propagations in flight
     (workspace = max_jobs * planes * N^2 * 8 bytes)."""
 
-    def __init__(self, cfg: OpticsConfig, max_jobs: int = 8, device: Optional[int] = None):
+    def __init__(self, cfg: OpticsConfig, max_jobs: int = 8, device: Optional[int] = None,
+                 precision: int = _lib.PRECISION_F32):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise RuntimeError("hbx.Plan needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -149,6 +150,8 @@ class Plan:
             _lib.check(self.lib.hbx_plan_create(C.byref(h), C.byref(oc), self.max_jobs,
                                                 self.device_index), "hbx_plan_create")
         self._h = h
+        if precision != _lib.PRECISION_F32:
+            self.precision = precision
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -177,6 +180,20 @@ class Plan:
         _lib.check(self.lib.hbx_plan_read_timing(self._h, ms, n, jobs), "hbx_plan_read_timing")
         names = _lib.PIPE_PASS_NAMES[self.pipeline]
         return {name: (ms[i], n[i], jobs[i]) for i, name in enumerate(names)}
+
+    @property
+    def precision(self) -> int:
+        """hbx_plan_precision: rounding of the pass intermediates (_lib.PRECISION_*)."""
+        rc = int(self.lib.hbx_plan_precision(self._h))
+        if rc < 0:
+            _lib.check(rc, "hbx_plan_precision")
+        return rc
+
+    @precision.setter
+    def precision(self, kind: int):
+        """PRECISION_F32 (the product path) or the bf16 / fp16 intermediate-storage
+        numerics of SURVEY 8d cfg 5 (DBS_ratio_0.5.py fp32 vs bf16 sweep)."""
+        _lib.check(self.lib.hbx_plan_set_precision(self._h, int(kind)), "hbx_plan_set_precision")
 
     @property
     def pipeline(self) -> int:
@@ -274,6 +291,9 @@ class Plan:
         """eval_flips on the incremental-field path: field [CH, H, W, 2] f32 and
         intensity [G, H, W] f32 of the base state (from simulate)."""
         c = self.cfg
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
         _need(field, "field", torch.float32, (c.channels, c.height, c.width, 2), self.device)
         _need(intensity, "intensity", torch.float32, (c.groups, c.height, c.width), self.device)
         k = flips.shape[0]
@@ -287,11 +307,31 @@ class Plan:
                                                _ptr(group_stats), _stream(stream)), "hbx_eval_flips_psf")
         return psnr_out, group_stats
 
+    def _check_commit(self, base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats, k_dev):
+        c = self.cfg
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
+        _need(prev_psnr, "prev_psnr", torch.float64, (1,), self.device)
+        k = flips.shape[0]
+        _need(flips, "flips", torch.int64, (k,), self.device)
+        if psnr_out.shape[0] < k or group_stats.shape[0] < k:
+            raise ValueError(f"psnr_out / group_stats hold fewer than the {k} candidates of flips")
+        _need(psnr_out, "psnr_out", torch.float64, (psnr_out.shape[0],), self.device)
+        _need(group_stats, "group_stats", torch.float64, (group_stats.shape[0], 3), self.device)
+        _need(k_dev, "k", torch.int32, (1,), self.device)
+        return k
+
     def commit_flip_psf(self, base_mask, base_stats, prev_psnr, field, intensity, flips, psnr_out,
                         group_stats, k_dev: torch.Tensor, stream=None):
+        """Commit candidate k_dev of an eval_flips_psf batch (a k outside the
+        batch commits nothing)."""
+        c = self.cfg
+        k = self._check_commit(base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats, k_dev)
+        _need(field, "field", torch.float32, (c.channels, c.height, c.width, 2), self.device)
+        _need(intensity, "intensity", torch.float32, (c.groups, c.height, c.width), self.device)
         _lib.check(self.lib.hbx_commit_flip_psf(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),
                                                 _ptr(field), _ptr(intensity), _ptr(flips), _ptr(psnr_out),
-                                                _ptr(group_stats), _ptr(k_dev), _stream(stream)),
+                                                _ptr(group_stats), _ptr(k_dev), k, _stream(stream)),
                    "hbx_commit_flip_psf")
 
     def dbs_walk_psf(self, base_mask, target, base_stats, field, intensity, order: torch.Tensor,
@@ -311,14 +351,18 @@ class Plan:
         _need(accept_pos, "accept_pos", torch.int64, (cap,), self.device)
         _need(accept_psnr, "accept_psnr", torch.float64, (cap,), self.device)
         _lib.check(self.lib.hbx_dbs_walk_psf(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
-                                             _ptr(field), _ptr(intensity), _ptr(order), _ptr(walk),
+                                             _ptr(field), _ptr(intensity), _ptr(order), int(order.shape[0]),
+                                             _ptr(walk),
                                              _ptr(accept_pos), _ptr(accept_psnr), cap, int(K), int(batches),
                                              _stream(stream)), "hbx_dbs_walk_psf")
 
     def commit_flip(self, base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats,
                     k_dev: torch.Tensor, stream=None):
+        """Commit candidate k_dev of an eval_flips batch (a k outside the batch
+        commits nothing)."""
+        k = self._check_commit(base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats, k_dev)
         _lib.check(self.lib.hbx_commit_flip(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),
-                                            _ptr(flips), _ptr(psnr_out), _ptr(group_stats), _ptr(k_dev),
+                                            _ptr(flips), _ptr(psnr_out), _ptr(group_stats), _ptr(k_dev), k,
                                             _stream(stream)), "hbx_commit_flip")
 
     def step(self, mask, actions, target, chan_stats, prev_psnr, accept_rule=_lib.ACCEPT_DBS,

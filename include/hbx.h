@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 5
+#define HBX_ABI_VERSION 6
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -212,10 +212,11 @@ int hbx_flip_map(hbx_plan_t plan, const uint64_t* mask, const float* target, flo
 /* Commit one accepted candidate of hbx_eval_flips into the base env:
  * toggle mask bit `flips[k]`, chan_stats[g] = group_stats[k], prev_psnr =
  * psnr_out[k].  Device-side; `k` is a device int32 (from the host or a
- * device search). */
+ * device search); K (ABI v6) is the length of flips / psnr_out / group_stats:
+ * a k outside [0, K) commits nothing. */
 int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stats,
                     double* prev_psnr, const int64_t* flips, const double* psnr_out,
-                    const double* group_stats, const int32_t* k, void* stream);
+                    const double* group_stats, const int32_t* k, int32_t K, void* stream);
 
 /* hbx_eval_flips / hbx_commit_flip on the incremental-field path: the base
  * env additionally carries its per-plane field [CH][H][W][2] and group
@@ -230,7 +231,7 @@ int hbx_eval_flips_psf(hbx_plan_t plan, const uint64_t* base_mask, const float* 
 int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stats,
                         double* prev_psnr, float* field, float* intensity, const int64_t* flips,
                         const double* psnr_out, const double* group_stats, const int32_t* k,
-                        void* stream);
+                        int32_t K, void* stream);
 
 /* Device-resident greedy DBS walk (ABI v5): the whole loop of DBS.py:247-294 /
  * DBS_1024_24.py:313-422 -- visit order[pos..], keep a flip iff PSNR strictly
@@ -249,7 +250,15 @@ int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_
  * counters zero at the start); the caller reads it back between calls.  When halt == 1
  * (after every refresh_every-th accept) the caller re-propagates field,
  * intensity and base_chan_stats exactly (hbx_simulate / hbx_propagate), sets
- * prev_psnr to the exact PSNR and clears halt. */
+ * prev_psnr to the exact PSNR and clears halt.
+ * n_order (ABI v6) is the length of `order`: the walk never visits past
+ * min(walk->total, n_order).
+ *
+ * Candidate evaluation is in increment form: each candidate's f64 partials
+ * are sum dI T and sum (2 I + dI) dI with dI = delta (2 Re(U conj h) +
+ * delta |h|^2) / P formed in f32 per pixel, added to base_chan_stats -- the
+ * decision carries the increment's own f32 precision (~1e-13 dB at 1024x24),
+ * not the rounding of full-image sums. */
 typedef struct hbx_dbs_walk {
   int64_t pos;             /* next position of `order` to visit                  */
   int64_t total;           /* positions to visit (order length or a prefix)      */
@@ -270,7 +279,7 @@ typedef struct hbx_dbs_walk {
 } hbx_dbs_walk_t;
 int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
                      double* base_chan_stats, float* field, float* intensity, const int64_t* order,
-                     hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                     int64_t n_order, hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
                      int64_t accept_cap, int32_t K, int32_t batches, void* stream);
 
 /* Incremental-field ("PSF") mode (reported separately from
@@ -291,6 +300,20 @@ int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_en
  * incremental updates; counters and PSNR history are left untouched). */
 int hbx_field_refresh(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
                       const int32_t* env_ids, int32_t n_ids, void* stream);
+
+/* Precision of the propagation intermediates (ABI v6; SURVEY 8d cfg 5,
+ * DBS_ratio_0.5.py fp32-vs-bf16 sweep).  HBX_PRECISION_F32 is the product
+ * path.  HBX_PRECISION_BF16_STORE / HBX_PRECISION_F16_STORE round every value
+ * written to the two pass intermediates (row spectrum, column-pass output) to
+ * bf16 / fp16 -- the numerics of half-width intermediate storage, measured
+ * against f32 by tools/precision_sweep.py and bench.py (layout and traffic
+ * stay f32).  N = 64 / 256 / 1024 three-pass path only (HBX_ERR_UNSUPPORTED
+ * elsewhere). */
+#define HBX_PRECISION_F32 0
+#define HBX_PRECISION_BF16_STORE 1
+#define HBX_PRECISION_F16_STORE 2
+int hbx_plan_set_precision(hbx_plan_t plan, int32_t precision);
+int hbx_plan_precision(hbx_plan_t plan);
 
 /* Optional device timing of the three propagation passes (hipEvents recorded
  * on the launch stream around every pass launch; not for graph capture).

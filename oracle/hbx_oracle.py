@@ -457,6 +457,97 @@ def dbs_greedy(env: OracleEnv, order: Sequence[int], stop_diff: Optional[float] 
     return np.array(accepted, bool), np.array(psnrs, np.float64), env.previous_psnr
 
 
+def single_pixel_field(cfg: OpticsConfig, g: int) -> np.ndarray:
+    """Field of one unit pixel at (0, 0) after tt.simulate: IFFT2(H_g) (complex128).
+
+    tt.simulate is linear in the field, so flipping pixel (c, r, col)
+    of group g adds delta * roll(h_g, (r, col)) to plane c's field, with
+    delta = +-1 (amplitude {0,1}) or -+2 (phase {+1,-1}) (env.py:170-172)."""
+    return np.fft.ifft2(cfg.transfer(g))
+
+
+class LinearGreedy:
+    """Greedy DBS (DBS_1024_24.py:313-422, accept iff psnr > previous, strict
+    :355) evaluated in float64 by linearity instead of re-propagating the
+    touched group per candidate: the per-plane fields U_c (complex128) are kept,
+    a candidate's field change is delta * h_g shifted to the pixel, and its
+    channel sums change by
+
+        d(sum I T)   = sum dI T,        d(sum I^2) = sum (2 I + dI) dI,
+        dI = (|U_c + delta h|^2 - |U_c|^2) / P = delta (2 Re(U_c conj h) + delta |h|^2) / P,
+
+    all exact in float64 (tests/test_oracle.py checks it against the
+    re-propagating OracleEnv.evaluate_flip).  This makes a 1024x1024x24 greedy
+    prefix of thousands of candidates tractable on the CPU (~25 ms per
+    candidate instead of two 8-plane 1024^2 FFT sets), which pins the GPU
+    accept sequence at the headline size (tests/golden/dbs_prefix_1024x24.npz)."""
+
+    def __init__(self, cfg: OpticsConfig, pre_model: np.ndarray, target: np.ndarray):
+        self.cfg = c = cfg
+        self.state = (np.asarray(pre_model, np.float32) >= 0.5).astype(np.int8)   # env.py:120
+        self.target = np.asarray(target, np.float64).reshape(c.groups, c.height, c.width)
+        self.vb = 1.0 if c.field_kind == FIELD_AMPLITUDE else -2.0
+        self.h = []
+        self.fields = np.empty((c.channels, c.height, c.width), np.complex128)
+        self.intensity = np.empty((c.groups, c.height, c.width), np.float64)
+        for g in range(c.groups):
+            tf = c.transfer(g)
+            self.h.append(np.fft.ifft2(tf))
+            sl = slice(g * c.planes, (g + 1) * c.planes)
+            u = propagate(mask_to_field(self.state[sl], c.field_kind), tf)
+            self.fields[sl] = u
+            self.intensity[g] = np.mean(u.real * u.real + u.imag * u.imag, axis=0)
+        self.stats = np.stack([chan_stats(self.intensity[g], self.target[g]) for g in range(c.groups)])
+        self.count = c.groups * c.height * c.width
+        self.initial_psnr = self.previous_psnr = self.psnr(self.stats)
+
+    def psnr(self, stats) -> float:
+        c = self.cfg
+        return psnr_from_stats(stats, self.count, c.rel_scale, c.peak)
+
+    def evaluate(self, action: int):
+        """(psnr after the flip, g, ch, delta, shifted h, dI, new stats); state unchanged."""
+        c = self.cfg
+        ch, r, col = (int(v) for v in decode_action(action, c.height, c.width))
+        g = ch // c.planes
+        delta = self.vb * (1.0 - 2.0 * float(self.state[ch, r, col]))
+        hs = np.roll(self.h[g], (r, col), axis=(0, 1))
+        u = self.fields[ch]
+        re = u.real * hs.real + u.imag * hs.imag
+        di = delta * (2.0 * re + delta * (hs.real * hs.real + hs.imag * hs.imag)) / c.planes
+        st = self.stats.copy()
+        st[g, 0] += float(np.dot(di.ravel(), self.target[g].ravel()))
+        st[g, 1] += float(np.dot((2.0 * self.intensity[g] + di).ravel(), di.ravel()))
+        return self.psnr(st), g, ch, delta, hs, di, st
+
+    def commit(self, action: int, ev) -> None:
+        c = self.cfg
+        _, g, ch, delta, hs, di, st = ev
+        _, r, col = (int(v) for v in decode_action(action, c.height, c.width))
+        self.state[ch, r, col] ^= 1                                       # DBS_1024_24.py:320
+        self.fields[ch] += delta * hs
+        self.intensity[g] += di
+        self.stats = st                                                   # :358-363
+        self.previous_psnr = ev[0]
+
+    def run(self, order: Sequence[int], stop_diff: Optional[float] = None):
+        """Returns (accepted flags, psnr per candidate, psnr change per candidate
+        = psnr - previous psnr at that candidate) over ``order``."""
+        accepted, psnrs, deltas = [], [], []
+        for a in order:
+            ev = self.evaluate(int(a))
+            ps = ev[0]
+            ok = ps > self.previous_psnr                                   # :355 (strict)
+            deltas.append(ps - self.previous_psnr)
+            if ok:
+                self.commit(int(a), ev)
+            accepted.append(ok)
+            psnrs.append(ps)
+            if stop_diff is not None and ps - self.initial_psnr >= stop_diff:   # DBS_ratio_0.5.py:366-372
+                break
+        return np.array(accepted, bool), np.array(psnrs, np.float64), np.array(deltas, np.float64)
+
+
 def probe_sweep(env: OracleEnv, flips: Sequence[int]):
     """Independent flip-evaluate-undo trials against the fixed base
     (DBS_1024_24-128.py:310-373, range.py:294-335, env_group.py:96-120).

@@ -51,12 +51,14 @@ int main(void) {
   CHECK(hbx_step(NULL, NULL, NULL, 0, NULL, NULL, NULL, NULL, NULL, 0, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_eval_flips(NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_eval_flips_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);
-  CHECK(hbx_commit_flip(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
-  CHECK(hbx_commit_flip_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
+  CHECK(hbx_commit_flip(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL) == HBX_ERR_INVALID);
+  CHECK(hbx_commit_flip_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_flip_map(NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
-  CHECK(hbx_dbs_walk_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, 1, 1, NULL) ==
+  CHECK(hbx_dbs_walk_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL) ==
         HBX_ERR_INVALID);
   CHECK(hbx_plan_pipeline(NULL) == HBX_ERR_INVALID);
+  CHECK(hbx_plan_set_precision(NULL, HBX_PRECISION_BF16_STORE) == HBX_ERR_INVALID);
+  CHECK(hbx_plan_precision(NULL) == HBX_ERR_INVALID);
   CHECK(hbx_plan_set_timing(NULL, 4) == HBX_ERR_INVALID);
   CHECK(hbx_plan_read_timing(NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_plan_workspace_bytes(NULL) == 0);

@@ -5,6 +5,7 @@ absent), so these vectors are the oracle's own float64 outputs on
 seeded inputs, plus the reference's stated known answers (env.py:228-229).
 They pin (a) the oracle against silent drift and (b) the HIP path in the
 -m gpu parity tests.  Run:  python tests/golden/make_golden.py
+(the headline-size DBS fixtures: python tests/golden/make_golden.py --large)
 """
 import os
 import sys
@@ -132,6 +133,44 @@ def env_group_trace(steps=260, k=512, seed=77):
             "params": np.array([250, 30.0, 1])}
 
 
+def dbs_prefix_large(cfg, n, seed=0, order_seed=3, stop_diff=None, n_probe=0):
+    """Greedy DBS at a full reference size by the float64 linear evaluator
+    (O.LinearGreedy): the accept sequence, every candidate's PSNR and its
+    PSNR change against the running base, over the first ``n`` candidates of
+    rng(order_seed).permutation(CH*N^2) of the seeded synthetic
+    image.  The inputs are regenerated from the seeds, so only the outputs
+    are stored."""
+    pre, tgt = O.synthetic_inputs(cfg, seed)
+    order = np.random.default_rng(order_seed).permutation(cfg.channels * cfg.height * cfg.width)
+    if n is not None:
+        order = order[:n]
+    lg = O.LinearGreedy(cfg, pre, tgt)
+    # PSNR change of the first n_probe candidates against the INITIAL state (no commits):
+    # pins each candidate's evaluation, accepted or not (probe sweep / eval_flips)
+    probe = np.array([lg.evaluate(int(a))[0] - lg.initial_psnr for a in order[:n_probe]], np.float64)
+    acc, ps, delta = lg.run(order, stop_diff=stop_diff)
+    return {"seed": np.int64(seed), "order_seed": np.int64(order_seed),
+            "size": np.int64(cfg.height), "groups": np.int64(cfg.groups), "planes": np.int64(cfg.planes),
+            "field_kind": np.int64(cfg.field_kind), "n": np.int64(len(acc)),
+            "stop_diff": np.float64(np.nan if stop_diff is None else stop_diff),
+            "accepted": acc, "psnr": ps, "delta": delta,
+            "initial_psnr": np.float64(lg.initial_psnr), "final_psnr": np.float64(lg.previous_psnr),
+            "probe_delta": probe}
+
+
+def build_large(only=()):
+    """The headline-size fixtures (minutes of CPU; not rebuilt by the CPU tests):
+    DBS_1024_24.py greedy prefixes (amplitude 4096 candidates, phase 1024) and the
+    literal DBS_ratio_0.5.py run (256x256x8 mono until +0.5 dB, :366-372)."""
+    specs = {
+        "dbs_prefix_1024x24.npz": lambda: dbs_prefix_large(O.rgb_config(1024), 4096, n_probe=512),
+        "dbs_prefix_1024x24_phase.npz":
+            lambda: dbs_prefix_large(O.rgb_config(1024, field_kind=O.FIELD_PHASE), 1024),
+        "dbs_ratio05_256.npz": lambda: dbs_prefix_large(O.mono_config(256), None, stop_diff=0.5),
+    }
+    return {k: f() for k, f in specs.items() if not only or k in only}
+
+
 def build_all():
     dt = decode_table()
     s, succ, maxs = reward_table()
@@ -148,7 +187,9 @@ def build_all():
 
 
 def main():
-    for name, arrays in build_all().items():
+    large = "--large" in sys.argv
+    only = [a for a in sys.argv[1:] if a.endswith(".npz")]
+    for name, arrays in (build_large(only) if large else build_all()).items():
         np.savez_compressed(os.path.join(HERE, name), **arrays)
         print("wrote", name)
 

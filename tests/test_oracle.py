@@ -244,3 +244,40 @@ def test_importance_values_match_reference_formula():
     # the polynomial passes through the reference's six anchor points
     from hbx.importance import rank_polynomial, STEP_POLY, REWARDS_POLY
     assert np.allclose(rank_polynomial()(STEP_POLY), REWARDS_POLY, atol=1e-9)
+
+
+@pytest.mark.parametrize("field_kind", [O.FIELD_AMPLITUDE, O.FIELD_PHASE])
+def test_linear_greedy_equals_repropagating_oracle(field_kind):
+    """O.LinearGreedy (increments by linearity of tt.simulate) reproduces the
+    re-propagating serial DBS (DBS_1024_24.py:313-422) decision for decision."""
+    cfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB, field_kind=field_kind)
+    pre, tgt = O.synthetic_inputs(cfg, 21)
+    env = O.OracleEnv(cfg, accept_rule=1)
+    env.reset(pre, tgt)
+    order = np.random.default_rng(3).permutation(cfg.channels * 64 * 64)[:400]
+    acc, ps, final = O.dbs_greedy(env, order)
+    lg = O.LinearGreedy(cfg, pre, tgt)
+    acc2, ps2, delta = lg.run(order)
+    assert np.array_equal(acc, acc2)
+    assert np.max(np.abs(ps - ps2)) <= 1e-12
+    assert np.max(np.abs(lg.intensity - env.intensity)) <= 1e-12
+    assert np.array_equal(lg.state, env.state)
+    assert abs(lg.previous_psnr - final) <= 1e-12
+
+
+@pytest.mark.parametrize("name,n_check", [("dbs_prefix_1024x24.npz", 12), ("dbs_ratio05_256.npz", 300)])
+def test_large_dbs_fixtures_reproduce(golden_dir, name, n_check):
+    """The headline-size DBS fixtures (make_golden.py --large) against a fresh
+    oracle run of their first candidates (the full runs take minutes)."""
+    import os
+    d = np.load(os.path.join(golden_dir, name), allow_pickle=False)
+    n, g = int(d["size"]), int(d["groups"])
+    cfg = O.OpticsConfig(n, n, g, int(d["planes"]), O.WL_RGB if g == 3 else O.WL_MONO,
+                         field_kind=int(d["field_kind"]))
+    pre, tgt = O.synthetic_inputs(cfg, int(d["seed"]))
+    order = np.random.default_rng(int(d["order_seed"])).permutation(cfg.channels * n * n)[:n_check]
+    lg = O.LinearGreedy(cfg, pre, tgt)
+    assert lg.initial_psnr == pytest.approx(float(d["initial_psnr"]), abs=1e-10)
+    acc, ps, delta = lg.run(order)
+    assert np.array_equal(acc, d["accepted"][:n_check])
+    assert np.allclose(delta, d["delta"][:n_check], rtol=0, atol=1e-12)
