@@ -159,11 +159,17 @@ class HologramVecEnv:
             self.action_space = spaces.MultiDiscrete([c.channels, c.height, c.width])
         else:
             self.action_space = spaces.Discrete(self.num_pixels)       # env.py:50-52
-        self.observation_space = spaces.Dict({                          # env.py:42-48
-            "state_record": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
+        # env.py:42-48 with the bounds the observations actually keep: the reference
+        # declares [0, 1] for state_record (a per-pixel int8 flip counter that wraps like
+        # numpy int8, env.py:165) and recon_image (a raw mean intensity |U|^2, > 1 at
+        # bright pixels, env.py:179), so its own observations fail its declared space;
+        # and env_1024_24.py:48-49 declare (1, N, N) for the RGB images it returns as
+        # (1, 3, N, N).  Shapes and dtypes -- what SB3's MultiInputPolicy reads -- match.
+        self.observation_space = spaces.Dict({
+            "state_record": spaces.Box(-128, 127, (1, c.channels, c.height, c.width), np.int8),
             "state": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.int8),
             "pre_model": spaces.Box(0, 1, (1, c.channels, c.height, c.width), np.float32),
-            "recon_image": spaces.Box(0, 1, (1, c.groups, c.height, c.width), np.float32),
+            "recon_image": spaces.Box(0, np.inf, (1, c.groups, c.height, c.width), np.float32),
             "target_image": spaces.Box(0, 1, (1, c.groups, c.height, c.width), np.float32),
         })
         n, dev = self.num_envs, self.device
@@ -359,17 +365,39 @@ def _to_numpy(obs: dict):
     return {k: v.detach().cpu().numpy() for k, v in obs.items()}
 
 
+def timing_lines(step: int, timing: dict) -> str:
+    """debug_env.py's per-phase timing lines (`:165-306`) for hbx_plan_read_timing's
+    pass times: "Step: N      | Time <pass>: s seconds", the format
+    log_py/debug_log.py:37-38 parses (one line per pass that ran)."""
+    out = []
+    for name, (ms, launches, _jobs) in timing.items():
+        if launches:
+            out.append(f"Step: {step:<6} | Time {name}: {ms * 1e-3:.6f} seconds")
+    return "\n".join(out)
+
+
 class BinaryHologramEnv(spaces.EnvBase):
     """Drop-in for the reference ``BinaryHologramEnv`` (env.py:37-259).
 
     target_function: pre-model (env.py:110); trainloader yields (target, path)
     (env.py:96-102).  ``config`` selects the optics: mono 256x256x8 (env.py)
     by default; pass ``rgb_config(1024)`` for env_1024_24.py.  Observations
-    are numpy dicts like the reference; scalars are Python floats."""
+    are numpy dicts shaped like the reference's -- state / state_record /
+    pre_model (1, CH, N, N), recon_image / target_image (1, G, N, N)
+    (env.py:135-140,176-181) -- and ``observation_space.contains`` accepts them;
+    scalars are Python floats.
+
+    verbose=True prints the reference's console lines (env.py:100,104,142-145:
+    episode start, initial PSNR / MSE; :203-246: a Step block at every 0.01 dB
+    threshold, at the T_PSNR_DIFF condition and at max_steps).  debug_timing=True
+    adds debug_env.py's per-phase lines (`Step: N | Time <phase>: s seconds`,
+    `:165-306`, parsed by log_py/debug_log.py:28-60): action, simulate, obs,
+    reward, rollback | print, diff, max_steps, terminated, plus the device time
+    of every propagation pass (hbx_plan_read_timing)."""
 
     def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
                  T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
-                 device: Optional[int] = None, **vec_kwargs):
+                 device: Optional[int] = None, debug_timing: bool = False, **vec_kwargs):
         super().__init__()
         self.cfg = config or mono_config(256)
         self.target_function = target_function
@@ -377,6 +405,7 @@ class BinaryHologramEnv(spaces.EnvBase):
         self.data_iter = iter(self.trainloader)
         self.max_steps, self.T_PSNR, self.T_steps, self.T_PSNR_DIFF = max_steps, T_PSNR, T_steps, T_PSNR_DIFF
         self.verbose = verbose
+        self.debug_timing = debug_timing
         self.current_file = None
         self._vec = HologramVecEnv(self.cfg, 1, self._next_target, self._pre_model, max_steps=max_steps,
                                    T_PSNR=T_PSNR, T_steps=T_steps, T_PSNR_DIFF=T_PSNR_DIFF,
@@ -390,15 +419,22 @@ class BinaryHologramEnv(spaces.EnvBase):
         self.steps = 0
         self.flip_count = 0
         self.psnr_sustained_steps = 0
+        self.max_psnr_diff = float("-inf")
+        self.next_print_thresholds = []
+        self.step_time = time.time()
+        if debug_timing:
+            self._vec.plan.set_timing(64)
 
     def _next_target(self, i):
         try:                                                           # env.py:96-102
             target, self.current_file = next(self.data_iter)
         except StopIteration:
-            if self.verbose:
-                print("\033[40;93m[INFO] Reached the end of dataset. Restarting from the beginning.\033[0m")
+            print("\033[40;93m[INFO] Reached the end of dataset. Restarting from the beginning.\033[0m")
             self.data_iter = iter(self.trainloader)
             target, self.current_file = next(self.data_iter)
+        if self.verbose:                                               # env.py:104
+            print(f"\033[40;93m[Episode Start] Currently using dataset file: {self.current_file}, "
+                  f"Episode count: {self.episode_num_count}\033[0m")
         return target
 
     def _pre_model(self, target):
@@ -410,28 +446,111 @@ class BinaryHologramEnv(spaces.EnvBase):
     def state(self):
         return unpack_bits(self._vec.state.mask[0], self.cfg.width).unsqueeze(0).cpu().numpy()
 
+    def _obs(self, stepped: bool) -> dict:
+        """The B = 1 batch axis of HologramVecEnv.observe() removed: (1, CH, N, N) /
+        (1, G, N, N) numpy arrays, the reference's obs dict (env.py:135-140,176-181)."""
+        return {k: v[0] for k, v in _to_numpy(self._vec.observe(stepped=stepped)).items()}
+
+    def _mse(self) -> float:
+        """tt.relativeLoss(result, target, F.mse_loss) of the current state (env.py:131)."""
+        st = self._vec.state.chan_stats[0].double().sum(0).cpu().numpy()
+        sxy, sxx, syy = (float(v) for v in st)
+        count = self.cfg.groups * self.cfg.height * self.cfg.width
+        if self.cfg.rel_scale == _lib.REL_LSQ:
+            return (syy - sxy * sxy / sxx) / count if sxx > 0 else syy / count
+        return (sxx - 2 * sxy + syy) / count
+
     def reset(self, seed=None, options=None):
         self.episode_num_count += 1
-        obs = _to_numpy(self._vec.reset())
+        self.psnr_sustained_steps = 0
+        obs = {k: v[0] for k, v in _to_numpy(self._vec.reset()).items()}
         self.initial_psnr = float(self._vec.state.init_psnr[0].item())
         self.previous_psnr = self.initial_psnr
         self.steps = self.flip_count = self.psnr_sustained_steps = 0
+        self.max_psnr_diff = float("-inf")
+        self.next_print_thresholds = [self.initial_psnr + i * 0.01 for i in range(1, 21)]   # env.py:148
+        if self.verbose:                                               # env.py:142-145
+            print(f"\033[92mInitial PSNR: {self.initial_psnr:.6f}\033[0m\nInitial MSE: {self._mse():.6f}\033[0m")
+        if self.debug_timing:
+            self._vec.plan.read_timing()                               # drop the reset's propagation
         self.total_start_time = time.time()
-        if self.verbose:
-            print(f"\033[92mInitial PSNR: {self.initial_psnr:.6f}\033[0m")
+        self.step_time = time.time()
         return obs, {"state": obs.get("state")}
 
+    def _flat_action(self, action) -> int:
+        return int(action)
+
+    def _block(self, psnr_after, change, diff, reward, ratio, c, r, col) -> str:
+        t = time.time() - self.total_start_time                       # env.py:206-212
+        return (f"Step: {self.steps:<6} | Initial PSNR: {self.initial_psnr:.6f}"
+                f"\nPSNR After: {psnr_after:.6f} | Change: {change:.6f} | Diff: {diff:.6f}"
+                f"\nReward: {reward:.2f} | Success Ratio: {ratio:.6f} | Flip Count: {self.flip_count}"
+                f"\nFlip Pixel: Channel={c}, Row={r}, Col={col}"
+                f"\nTime taken for this data: {t:.2f} seconds")
+
     def step(self, action):
-        a = torch.tensor([int(action)], dtype=torch.int64, device=self._vec.device)
-        reward, psnr, acc, term, trunc = self._vec.step_device(a)
-        self._vec.state.check_error()
-        obs = _to_numpy(self._vec.observe(stepped=True))
+        dbg = self.debug_timing
+        if dbg:
+            print(f"Step: {self.steps + 1:<6} | Time action: {time.time() - self.step_time:.6f} seconds")
+        a = self._flat_action(action)
+        t0 = time.time()
+        reward_t, psnr_t, acc_t, term_t, trunc_t = self._vec.step_device(
+            torch.tensor([a], dtype=torch.int64, device=self._vec.device))
+        self._vec.state.check_error()                                  # syncs the step
+        if dbg:
+            print(f"Step: {self.steps + 1:<6} | Time simulate: {time.time() - t0:.6f} seconds")
+        t0 = time.time()
+        obs = self._obs(stepped=True)
+        if dbg:
+            print(f"Step: {self.steps + 1:<6} | Time obs: {time.time() - t0:.6f} seconds")
+        t0 = time.time()
         st = self._vec.state
+        prev = self.previous_psnr
+        reward = float(reward_t[0].item())
+        psnr_after = float(psnr_t[0].item())
+        accepted = bool(acc_t[0].item())
+        terminated, truncated = bool(term_t[0].item()), bool(trunc_t[0].item())
         self.steps = int(st.steps[0].item())
         self.flip_count = int(st.flip_count[0].item())
         self.psnr_sustained_steps = int(st.sustained[0].item())
         self.previous_psnr = float(st.prev_psnr[0].item())
-        return obs, float(reward[0].item()), bool(term[0].item()), bool(trunc[0].item()), {}
+        if dbg:
+            print(f"Step: {self.steps:<6} | Time reward: {time.time() - t0:.6f} seconds")
+            print(timing_lines(self.steps, self._vec.plan.read_timing()))
+        if not accepted:                                               # env.py:191-196 (rolled back on the device)
+            if dbg:
+                print(f"Step: {self.steps:<6} | Time rollback: {0.0:.6f} seconds")
+                self.step_time = time.time()
+            return obs, reward, False, False, {}
+        change, diff = psnr_after - prev, psnr_after - self.initial_psnr
+        self.max_psnr_diff = max(self.max_psnr_diff, diff)
+        ratio = self.flip_count / self.steps if self.steps > 0 else 0
+        c, r, col = (int(v) for v in np.unravel_index(a, (self.cfg.channels, self.cfg.height, self.cfg.width)))
+        base_reward = change * self._vec.params.reward_weight
+        t0 = time.time()
+        while self.next_print_thresholds and psnr_after >= self.next_print_thresholds[0]:   # env.py:203-212
+            self.next_print_thresholds.pop(0)
+            if self.verbose:
+                print(self._block(psnr_after, change, diff, base_reward, ratio, c, r, col))
+        if dbg:
+            print(f"Step: {self.steps:<6} | Time print: {time.time() - t0:.6f} seconds")
+        t0 = time.time()
+        bonus = 0.0
+        if diff >= self.T_PSNR_DIFF or (psnr_after >= self.T_PSNR and diff < 0.1):          # env.py:216-235
+            if self.verbose:
+                print(self._block(psnr_after, change, diff, base_reward, ratio, c, r, col))
+            if self.psnr_sustained_steps >= self.T_steps and diff >= self.T_PSNR_DIFF:
+                bonus = reward - base_reward
+        if dbg:
+            print(f"Step: {self.steps:<6} | Time diff: {time.time() - t0:.6f} seconds")
+        t0 = time.time()
+        if self.steps >= self.max_steps and self.verbose:                                   # env.py:237-246
+            print(self._block(psnr_after, change, diff, base_reward + bonus, ratio, c, r, col))
+        if dbg:
+            print(f"Step: {self.steps:<6} | Time max_steps: {time.time() - t0:.6f} seconds")
+            print(f"Step: {self.steps:<6} | Time terminated: {0.0:.6f} seconds")
+            self.step_time = time.time()
+        return obs, reward, terminated, truncated, {}
 
     def close(self):
         self._vec.close()
@@ -474,17 +593,15 @@ class BinaryHologramEnvMD(BinaryHologramEnv):
                  T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
                  device: Optional[int] = None):
         super().__init__(target_function, trainloader, max_steps=max_steps, T_PSNR=T_PSNR, T_steps=T_steps,
-                         T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device,
-                         action_format="multidiscrete")
+                         T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device)
+        c = self.cfg
+        self.action_space = spaces.MultiDiscrete([c.channels, c.height, c.width])   # env_md.py:54
 
-    def step(self, action):
-        a = torch.as_tensor(np.asarray(action, np.int64).reshape(1, 3), device=self._vec.device)
-        reward, psnr, acc, term, trunc = self._vec.step_device(a)
-        self._vec.state.check_error()
-        obs = _to_numpy(self._vec.observe(stepped=True))
-        st = self._vec.state
-        self.steps = int(st.steps[0].item())
-        self.flip_count = int(st.flip_count[0].item())
-        self.psnr_sustained_steps = int(st.sustained[0].item())
-        self.previous_psnr = float(st.prev_psnr[0].item())
-        return obs, float(reward[0].item()), bool(term[0].item()), bool(trunc[0].item()), {}
+    def _flat_action(self, action) -> int:
+        """env_md.py:159 `channel, row, col = action` -> the flat index env.py decodes;
+        out of range components raise like the Discrete env."""
+        c, r, col = (int(v) for v in np.asarray(action, np.int64).reshape(3))
+        cfg = self.cfg
+        if not (0 <= c < cfg.channels and 0 <= r < cfg.height and 0 <= col < cfg.width):
+            raise ValueError(f"action {(c, r, col)} outside MultiDiscrete({[cfg.channels, cfg.height, cfg.width]})")
+        return (c * cfg.height + r) * cfg.width + col

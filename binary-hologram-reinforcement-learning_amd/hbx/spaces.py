@@ -87,6 +87,13 @@ class Dict(_Space):
     def sample(self):
         return {k: s.sample() for k, s in self.spaces.items()}
 
+    def contains(self, x):
+        return isinstance(x, dict) and set(x) == set(self.spaces) and \
+            all(s.contains(x[k]) for k, s in self.spaces.items())
+
+    def __repr__(self):
+        return "Dict(" + ", ".join(f"{k}: {s!r}" for k, s in self.spaces.items()) + ")"
+
 
 if HAVE_GYMNASIUM:  # pragma: no cover
     Box, Discrete, MultiDiscrete, Dict = _spaces.Box, _spaces.Discrete, _spaces.MultiDiscrete, _spaces.Dict

@@ -1,0 +1,256 @@
+"""The drop-in env classes (hbx.env.BinaryHologramEnv / Group / MD) under the
+reference's own contracts, and the literal DBS_1024_24.py driver statements
+running against them through the torchOptics shim.
+
+Reference contracts checked:
+  env.py:42-52      observation_space Dict / Discrete action_space
+  env.py:135-140    reset obs: state / state_record / pre_model (1, CH, N, N),
+                    recon_image / target_image (1, G, N, N); info {"state": ...}
+  env.py:154-259    step -> (obs, reward float, terminated bool, truncated bool, {})
+  env_md.py:54,160  MultiDiscrete([CH, N, N]) actions
+  DBS_1024_24.py:221-422  the driver reads obs["state"].shape[1], slices colour
+                    groups, propagates them with tt.simulate, caches the group
+                    means and runs the greedy loop on current_state[0, c, r, col]
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import hbx_oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    import hbx
+    hbx.load_library()
+    yield
+
+
+class _Loader:
+    """A DataLoader(batch_size=1) stand-in: (target [1, G, N, N], [path]) items."""
+
+    def __init__(self, targets):
+        self.targets = targets
+
+    def __iter__(self):
+        for i, t in enumerate(self.targets):
+            yield torch.from_numpy(t[None]), [f"/data/valid/{801 + i:04d}.png"]
+
+
+def _setup(ocfg, n_images=2, seed=40):
+    ins = [O.synthetic_inputs(ocfg, seed + 2 * i) for i in range(n_images)]
+    pres = {float(t[0, 0, 0]): p for p, t in ins}     # target -> pre-model output (BinaryNet stand-in)
+
+    def target_function(target):
+        key = float(target.reshape(-1)[0])
+        return torch.from_numpy(pres[key][None]).to(target.device)
+
+    return _Loader([t for _, t in ins]), target_function, ins
+
+
+def _dev_cfg(ocfg):
+    import hbx
+    return hbx.OpticsConfig(ocfg.height, ocfg.width, ocfg.groups, ocfg.planes, tuple(ocfg.wavelengths))
+
+
+@pytest.mark.parametrize("rgb", [False, True])
+def test_binary_hologram_env_contract_and_trace(rgb, capsys):
+    from hbx.env import BinaryHologramEnv
+    ocfg = O.OpticsConfig(64, 64, 3, 8, O.WL_RGB) if rgb else O.mono_config(64)
+    loader, tf, ins = _setup(ocfg)
+    env = BinaryHologramEnv(tf, loader, max_steps=30, T_PSNR_DIFF=0.05, config=_dev_cfg(ocfg), verbose=True)
+    obs, info = env.reset()
+    CH, G, N = ocfg.channels, ocfg.groups, 64
+    shapes = {"state": (1, CH, N, N), "state_record": (1, CH, N, N), "pre_model": (1, CH, N, N),
+              "recon_image": (1, G, N, N), "target_image": (1, G, N, N)}
+    assert {k: v.shape for k, v in obs.items()} == shapes
+    assert obs["state"].dtype == np.int8 and obs["pre_model"].dtype == np.float32
+    assert env.observation_space.contains(obs)
+    assert np.array_equal(info["state"], obs["state"])
+    pre, tgt = ins[0]
+    assert np.array_equal(obs["state"][0], (pre >= 0.5).astype(np.int8))       # env.py:120
+    assert np.allclose(obs["target_image"][0], tgt)
+    oe = O.OracleEnv(ocfg, max_steps=30, T_PSNR_DIFF=0.05)
+    oe.reset(pre, tgt)
+    assert abs(env.initial_psnr - oe.initial_psnr) <= 1e-4
+    rng = np.random.default_rng(5)
+    for _ in range(30):
+        a = int(rng.integers(0, env.action_space.n))
+        obs, reward, term, trunc, info = env.step(a)
+        want = oe.step(a)
+        assert isinstance(reward, float) and isinstance(term, bool) and isinstance(trunc, bool) and info == {}
+        assert env.observation_space.contains(obs)
+        assert abs(reward - want.reward) <= 800 * 2e-4
+        assert (term, trunc) == (want.terminated, want.truncated)
+        assert np.array_equal(obs["state"][0], oe.state)                        # rollback applied
+        assert env.previous_psnr == pytest.approx(oe.previous_psnr, abs=1e-4)
+        if term or trunc:
+            break
+    out = capsys.readouterr().out
+    # the DataLoader yields a batch of paths, printed as the list (env.py:104 formats current_file as is)
+    assert "[Episode Start] Currently using dataset file: ['/data/valid/0801.png'], Episode count: 1" in out
+    assert "PSNR After:" in out and "| Flip Count:" in out                      # env.py:206-212 blocks
+    assert "Initial PSNR:" in out and "Initial MSE:" in out
+    env.close()
+
+
+def test_debug_timing_lines_parse(capsys):
+    """debug_env.py's per-phase timing lines, in the format log_py/debug_log.py:37-38 parses."""
+    import re
+    from hbx.env import BinaryHologramEnv
+    ocfg = O.mono_config(64)
+    loader, tf, _ = _setup(ocfg, 1)
+    env = BinaryHologramEnv(tf, loader, config=_dev_cfg(ocfg), debug_timing=True)
+    env.reset()
+    for a in (3, 4000, 70000 % (8 * 4096)):
+        env.step(a)
+    out = capsys.readouterr().out
+    rx = re.compile(r"Step:\s*(\d+)\s*\|\s*Time\s*(.+?)\s*:\s*([\d\.]+)\s*seconds")
+    phases = {m.group(2) for m in rx.finditer(out)}
+    assert {"action", "simulate", "obs", "reward", "k_rowfwd", "k_col", "k_rowinv"} <= phases
+    assert {int(m.group(1)) for m in rx.finditer(out)} == {1, 2, 3}
+    env.close()
+
+
+def test_group_and_md_contracts():
+    from hbx.env import BinaryHologramEnvGroup, BinaryHologramEnvMD
+    ocfg = O.mono_config(64)
+    loader, tf, ins = _setup(ocfg)
+    g = BinaryHologramEnvGroup(tf, loader, config=_dev_cfg(ocfg), importance_samples=256)
+    obs, info = g.reset()
+    assert g.observation_space.contains(obs) and obs["state"].shape == (1, 8, 64, 64)
+    assert g.psnr_change_list.shape == (256,) and g.importance_ranks.shape == (256,)
+    obs, r, term, trunc, info = g.step(17)
+    assert g.observation_space.contains(obs) and isinstance(r, float)
+    g.close()
+    loader, tf, ins = _setup(ocfg)
+    md = BinaryHologramEnvMD(tf, loader, config=_dev_cfg(ocfg), max_steps=10)
+    obs, _ = md.reset()
+    assert list(md.action_space.nvec) == [8, 64, 64]
+    oe = O.OracleEnv(ocfg, max_steps=10)
+    oe.reset(*ins[0])
+    rng = np.random.default_rng(9)
+    for _ in range(10):
+        c, r, col = int(rng.integers(8)), int(rng.integers(64)), int(rng.integers(64))
+        obs, rew, term, trunc, _ = md.step((c, r, col))                       # env_md.py:159
+        want = oe.step(int(O.encode_action(c, r, col, 64, 64)))
+        assert md.observation_space.contains(obs)
+        assert abs(rew - want.reward) <= 800 * 2e-4 and (term, trunc) == (want.terminated, want.truncated)
+    with pytest.raises(ValueError):
+        md.step((8, 0, 0))
+    md.close()
+
+
+def test_dbs_1024_24_driver_statements_unchanged():
+    """DBS_1024_24.py:221-422, statement for statement (np.random.shuffle replaced
+    by a seeded permutation, prints and .npy saves left out), on the drop-in env
+    and the torchOptics shim at 64x64 with 3 groups x 8 planes.  The accept
+    sequence equals the float64 oracle's greedy DBS except at a candidate whose
+    PSNR change is below the f32 resolution of a full-image PSNR (1e-6 dB),
+    after which the comparison stops."""
+    import torchOptics.metrics as tm
+    import torchOptics.optics as tt
+    from hbx.env import BinaryHologramEnv
+    ocfg = O.OpticsConfig(64, 64, 3, 8, O.WL_RGB)
+    loader, tf, ins = _setup(ocfg, 1, seed=60)
+    env = BinaryHologramEnv(tf, loader, config=_dev_cfg(ocfg))
+    z, pixel_pitch = 2e-3, 7.56e-6
+
+    obs, info = env.reset()                                                      # :213
+    current_state = obs["state"]                                                 # :221
+    target_image = obs["target_image"]
+    target_image_cuda = torch.tensor(target_image, dtype=torch.float32).cuda()
+    initial_psnr = env.initial_psnr
+    previous_psnr = initial_psnr
+    steps = 0
+    flip_count = 0
+    meta = {'wl': (638e-9, 515e-9, 450e-9), 'dx': (pixel_pitch, pixel_pitch)}    # :230-233
+    rmeta = {'wl': (638e-9), 'dx': (pixel_pitch, pixel_pitch)}
+    gmeta = {'wl': (515e-9), 'dx': (pixel_pitch, pixel_pitch)}
+    bmeta = {'wl': (450e-9), 'dx': (pixel_pitch, pixel_pitch)}
+    rgbchannel = current_state.shape[1]                                          # :235
+    rchannel = int(rgbchannel / 3)
+    gchannel = int(rgbchannel * 2 / 3)
+    red = current_state[:, :rchannel, :, :]
+    green = current_state[:, rchannel:gchannel, :, :]
+    blue = current_state[:, gchannel:, :, :]
+    red = tt.Tensor(red, meta=rmeta)
+    green = tt.Tensor(green, meta=gmeta)
+    blue = tt.Tensor(blue, meta=bmeta)
+    rsim = tt.simulate(red, z).abs() ** 2                                        # :248-250
+    gsim = tt.simulate(green, z).abs() ** 2
+    bsim = tt.simulate(blue, z).abs() ** 2
+    rmean = torch.mean(rsim, dim=1, keepdim=True)
+    gmean = torch.mean(gsim, dim=1, keepdim=True)
+    bmean = torch.mean(bsim, dim=1, keepdim=True)
+    rgb = torch.cat([rmean, gmean, bmean], dim=1)
+    rgb = tt.Tensor(rgb, meta=meta)
+    assert tt.relativeLoss(rgb, target_image_cuda, tm.get_PSNR) == pytest.approx(initial_psnr, abs=1e-5)
+    a, imgname = next(iter(env.trainloader))                                     # :271
+    assert imgname[0].endswith("0801.png")
+
+    num_channels, img_height, img_width = current_state.shape[1:]                # :309
+    all_pixels = np.random.default_rng(3).permutation(num_channels * img_height * img_width)[:400]
+    accepted = []
+    for attempt, pixel in enumerate(all_pixels):                                 # :313-422
+        channel = pixel // (img_height * img_width)
+        pixel_index = pixel % (img_height * img_width)
+        row = pixel_index // img_width
+        col = pixel_index % img_width
+        current_state[0, channel, row, col] = 1 - current_state[0, channel, row, col]
+        steps += 1
+        if channel < 8:
+            red_after = current_state[:, :rchannel, :, :]
+            red_after = tt.Tensor(red_after, meta=rmeta)
+            rsim_after = tt.simulate(red_after, z).abs() ** 2
+            rmean_after = torch.mean(rsim_after, dim=1, keepdim=True)
+            rgb = torch.cat([rmean_after, gmean, bmean], dim=1)
+            rgb = tt.Tensor(rgb, meta=meta)
+            psnr_after = tt.relativeLoss(rgb, target_image_cuda, tm.get_PSNR)
+        elif 8 <= channel < 16:
+            green_after = current_state[:, rchannel:gchannel, :, :]
+            green_after = tt.Tensor(green_after, meta=gmeta)
+            gsim_after = tt.simulate(green_after, z).abs() ** 2
+            gmean_after = torch.mean(gsim_after, dim=1, keepdim=True)
+            rgb = torch.cat([rmean, gmean_after, bmean], dim=1)
+            rgb = tt.Tensor(rgb, meta=meta)
+            psnr_after = tt.relativeLoss(rgb, target_image_cuda, tm.get_PSNR)
+        elif 16 <= channel:
+            blue_after = current_state[:, gchannel:, :, :]
+            blue_after = tt.Tensor(blue_after, meta=bmeta)
+            bsim_after = tt.simulate(blue_after, z).abs() ** 2
+            bmean_after = torch.mean(bsim_after, dim=1, keepdim=True)
+            rgb = torch.cat([rmean, gmean, bmean_after], dim=1)
+            rgb = tt.Tensor(rgb, meta=meta)
+            psnr_after = tt.relativeLoss(rgb, target_image_cuda, tm.get_PSNR)
+        if psnr_after > previous_psnr:                                           # :355
+            flip_count += 1
+            if channel < 8:
+                rmean = rmean_after
+            elif 8 <= channel < 16:
+                gmean = gmean_after
+            elif 16 <= channel:
+                bmean = bmean_after
+            previous_psnr = psnr_after                                           # :418
+            accepted.append(True)
+        else:
+            current_state[0, channel, row, col] = 1 - current_state[0, channel, row, col]   # :422
+            accepted.append(False)
+
+    pre, tgt = ins[0]
+    lg = O.LinearGreedy(ocfg, pre, tgt)
+    want, _, delta = lg.run(all_pixels)
+    got = np.array(accepted)
+    diff = np.nonzero(got != want)[0]
+    upto = len(want) if len(diff) == 0 else int(diff[0])
+    if len(diff):
+        assert abs(delta[upto]) <= 1e-6, (upto, delta[upto])
+    assert upto >= 200 and flip_count > 50
+    if len(diff) == 0:
+        assert np.array_equal(current_state[0], lg.state)
+        assert previous_psnr == pytest.approx(lg.previous_psnr, abs=1e-5)
+    env.close()
