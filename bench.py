@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")
     ap.add_argument("--no-probe", action="store_true", help="skip the all-flip probe-sweep measurement")
     ap.add_argument("--no-ppo", action="store_true", help="skip the 256x256x8 mono (train-PPO) measurement")
+    ap.add_argument("--no-precision", action="store_true",
+                    help="skip the fp32-vs-bf16 intermediate-storage deviation (SURVEY 8d cfg 5)")
+    ap.add_argument("--gather-every", type=int, default=1,
+                    help="world > 1: steps of per-env metrics per gather to rank 0 (hbx.dist.StepMetricGather)")
     return ap.parse_args()
 
 
@@ -155,16 +159,33 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     r3 = dbs.greedy(plan, m3, target, order, mode="psf_host")
     torch.cuda.synchronize()
     dt3 = time.perf_counter() - t0
-    plan.close()
     a1 = np.zeros(n_flips, bool)
     a2 = np.zeros(n_flips, bool)
     a1[res.accepted_positions] = True
     a2[r2.accepted_positions] = True
     diff = np.nonzero(a1 != a2)[0]
+    first_change = None
+    if len(diff):
+        # both runs saw the same state up to the first differing candidate: replay it with the
+        # incremental walk and evaluate that candidate's PSNR change in increment form
+        # (resolved to ~1e-12 dB, tests/test_gpu_dbs_headline.py) -- a tie of the FFT mode's
+        # f32 resolution (~1e-9 dB per candidate) or a real disagreement
+        f = int(diff[0])
+        m4 = mask.clone()
+        if f > 0:
+            dbs.greedy(plan, m4, target, order[:f], mode="psf")
+        _, st4, p4 = plan.propagate(m4.unsqueeze(0), target.unsqueeze(0), want_intensity=False)
+        fc4, it4 = plan.simulate(m4.unsqueeze(0), want_intensity=True)
+        cand = torch.as_tensor(order[f:f + 1]).to(plan.device)
+        ps4, _ = plan.eval_flips_psf(m4, target, st4[0].contiguous(), torch.view_as_real(fc4[0]).contiguous(),
+                                     it4[0].contiguous(), cand)
+        first_change = float((ps4 - p4).item())
+    plan.close()
     out["incremental_mode"] = {"flips": r2.steps, "seconds": round(dt2, 3),
                                "flips_per_s": round(r2.steps / dt2, 1), "accepted": len(r2.accepted_positions),
                                "same_accepts_as_fft_mode": bool(len(diff) == 0),
                                "first_decision_difference": int(diff[0]) if len(diff) else None,
+                               "first_difference_change_db": first_change,
                                "decisions_differing": int(len(diff)),
                                "psnr_gain_db": round(r2.final_psnr - r2.initial_psnr, 6),
                                "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1),
@@ -176,9 +197,70 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                                    "batches": r3.launches,
                                    "same_accepts_as_device_walk": r3.accepted_positions == r2.accepted_positions,
                                    "note": "hbx_eval_flips_psf + host decision + hbx_commit_flip_psf per batch"},
-                               "note": "a flip moves the 1024x24 PSNR by a median 6.5e-7 dB "
-                                       "(profiles/r01_precision_cfg5.json); the two f32 paths can order "
-                                       "near-ties differently, after which the greedy sequences diverge"}
+                               "note": "a flip moves the 1024x24 PSNR by a median 6.7e-7 dB; the incremental "
+                                       "walk resolves a candidate's change to ~1e-12 dB (increment-form f64 "
+                                       "sums) and equals the float64 oracle's accept sequence on the committed "
+                                       "4096-candidate 1024x24 prefix, while the FFT mode (the reference's "
+                                       "algorithm in f32) resolves ~1e-9 dB, so the two can order a near-tie "
+                                       "differently (first_difference_change_db), after which the greedy "
+                                       "sequences visit different states"}
+    return out
+
+
+def precision_sweep(mask1024, target1024, n_flips: int = 2048):
+    """SURVEY 8d cfg 5 (BASELINE configs[4]): DBS_ratio_0.5.py's literal run -- 256x256x8
+    mono greedy DBS until the PSNR has risen 0.5 dB (:366-372), FFT mode -- with f32 and
+    with bf16-rounded pass intermediates (hbx_plan_set_precision), plus the per-flip PSNR
+    change of n_flips random flips of the 1024x24 bench state under both."""
+    import numpy as np
+    import torch
+    from hbx import dbs, pack_bits, PRECISION_BF16_STORE, PRECISION_F32
+    from hbx.plan import Plan, mono_config, rgb_config
+    mono = mono_config(256)
+    pre = np.random.default_rng(0).random((8, 256, 256), np.float32)     # SURVEY 8d seeds
+    tgt = np.random.default_rng(1).random((1, 256, 256), np.float32)
+    order = np.random.default_rng(3).permutation(8 * 256 * 256)
+    runs = {}
+    for name, prec in (("f32", PRECISION_F32), ("bf16", PRECISION_BF16_STORE)):
+        plan = Plan(mono, max_jobs=256, precision=prec)
+        mask = pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+        t0 = time.perf_counter()
+        res = dbs.greedy(plan, mask, torch.from_numpy(tgt).cuda(), order, stop_diff=0.5, mode="fft")
+        torch.cuda.synchronize()
+        runs[name] = (res, time.perf_counter() - t0)
+        plan.close()
+    (r32, t32), (rbf, tbf) = runs["f32"], runs["bf16"]
+    a32 = np.zeros(len(order), bool)
+    abf = np.zeros(len(order), bool)
+    a32[r32.accepted_positions] = True
+    abf[rbf.accepted_positions] = True
+    d = np.nonzero(a32 != abf)[0]
+    out = {"workload": "DBS_ratio_0.5.py: 256x256x8 mono greedy DBS (seeds 0/1/3) until +0.5 dB, FFT mode",
+           "f32": {"candidates": r32.steps, "accepts": len(r32.accepted_positions),
+                   "initial_psnr": r32.initial_psnr, "final_psnr": r32.final_psnr, "seconds": round(t32, 3)},
+           "bf16_intermediates": {"candidates": rbf.steps, "accepts": len(rbf.accepted_positions),
+                                  "initial_psnr": rbf.initial_psnr, "final_psnr": rbf.final_psnr,
+                                  "seconds": round(tbf, 3)},
+           "initial_psnr_deviation_db": abs(rbf.initial_psnr - r32.initial_psnr),
+           "final_psnr_deviation_db": abs(rbf.final_psnr - r32.final_psnr),
+           "first_accept_sequence_difference": int(d[0]) if len(d) else None}
+    cfg = rgb_config(1024)
+    flips = torch.from_numpy(np.random.default_rng(4).integers(0, 24 * 1024 * 1024, n_flips)).cuda()
+    deltas = {}
+    for name, prec in (("f32", PRECISION_F32), ("bf16", PRECISION_BF16_STORE)):
+        plan = Plan(cfg, max_jobs=256, precision=prec)
+        _, st, p0 = plan.propagate(mask1024.unsqueeze(0), target1024.unsqueeze(0), want_intensity=False)
+        ps, _ = plan.eval_flips(mask1024, target1024, st[0].contiguous(), flips)
+        deltas[name] = (ps - p0).cpu().numpy()
+        plan.close()
+    e = deltas["bf16"] - deltas["f32"]
+    out["per_flip_change_1024x24"] = {
+        "flips": n_flips, "median_abs_change_db": float(np.median(np.abs(deltas["f32"]))),
+        "bf16_rms_error_db": float(np.sqrt(np.mean(e * e))), "bf16_max_error_db": float(np.max(np.abs(e))),
+        "bf16_sign_errors": float(np.mean(np.sign(deltas["bf16"]) != np.sign(deltas["f32"])))}
+    out["note"] = ("bf16 rounding of the stored intermediates (numerics only; layout and traffic stay f32). "
+                   "The f32 path equals the float64 oracle's accept sequence on this run "
+                   "(tests/test_gpu_dbs_headline.py::test_dbs_ratio05_256_literal_run)")
     return out
 
 
@@ -253,11 +335,15 @@ def load_pmc_traffic(N: int = 1024):
         return None
 
 
-def pass_table(timing, abytes):
+def pass_table(timing, abytes, jobs_override=None):
+    """Per-pass average launch time and algorithmic GB/s.  jobs_override[name] replaces
+    the jobs a pass is charged for (k_psf_commit only rewrites the ACCEPTED envs' planes)."""
     passes = {}
     for name, (ms, launches, jobs) in timing.items():
         if launches:
             avg = ms / launches
+            if jobs_override and name in jobs_override:
+                jobs = jobs_override[name]
             per_launch = abytes[name] * (jobs / launches)
             passes[name] = {"avg_ms": avg, "launches": launches, "jobs_per_launch": jobs / launches,
                             "alg_bytes_per_launch": per_launch,
@@ -318,29 +404,38 @@ def main():
         gen = torch.Generator(device="cuda").manual_seed(2 + 7919 * rank)
         total = warmup + steps
         actions = torch.randint(0, mCH * mN * mN, (total, B), generator=gen, device="cuda", dtype=torch.int64)
+        mg = hd.StepMetricGather(B, args.gather_every, dev) if gather else None
 
         def one_step(k):
             r, ps, acc, term, trunc = vec.step_device(actions[k])
-            if gather:
-                hd.gather_to_rank0(hd.pack_step_metrics(r, ps, acc, term, trunc))
+            if mg is not None:
+                mg.add(r, ps, acc, term, trunc)
 
         for k in range(warmup):
             one_step(k)
+        if mg is not None:
+            mg.flush()
         torch.cuda.synchronize()
         vec.plan.set_timing(steps * -(-B // (args.chunk or B)) + 1)
         hd.barrier()
         torch.cuda.synchronize()
+        acc0 = int(vec.state.flip_count.sum().item())
         t0 = time.perf_counter()
         for k in range(warmup, total):
             one_step(k)
+        if mg is not None:
+            mg.flush()
         torch.cuda.synchronize()
         hd.barrier()
         dt = hd.max_over_ranks(time.perf_counter() - t0, dev)
         timing = vec.plan.read_timing()
         vec.state.check_error()
+        # accepted steps in the timed region (flip_count counts accepted flips, no resets here)
+        vec.timed_accepts = int(vec.state.flip_count.sum().item()) - acc0
         acc_rate = float(vec.state.flip_count.sum().item()) / float(vec.state.steps.sum().item())
         return vec, dt, timing, acc_rate
 
+    ranks_seen = hd.describe_world(dev)
     vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup)
     value = B * world * args.steps / dt
     ms_per_step = dt / args.steps * 1e3
@@ -380,7 +475,14 @@ def main():
                                    "(3 colour groups x 8 planes), one action per env per step, FFT mode "
                                    "(whole touched group re-propagated)",
                        "envs_per_gpu": B, "global_envs": B * world, "size": N, "planes": CH,
-                       "parallelism": f"env-sharded x{world}" + (" + RCCL metric gather" if gather else "")},
+                       "parallelism": f"env-sharded x{world}" + (
+                           f" + metric gather to rank 0 every {args.gather_every} step(s)" if gather else ""),
+                       "obs_keys": [],
+                       "obs_note": "the timed step returns reward / psnr / accepted / terminated / truncated "
+                                   "on the device; no observation is assembled (HologramVecEnv(obs_keys=())): "
+                                   "the recon_image write would add 4 N^2 B per env-step (~1.5 % of the "
+                                   "step's 273.7 MB canonical traffic)"},
+            "ranks_seen": ranks_seen,
             "roofline": roofline,
             "passes": rounded(passes),
             "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
@@ -405,11 +507,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_probe:
         out["probe_sweep"] = probe_sweep(cfg, dbs_mask, dbs_target)
         torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_precision and N == 1024:
+        out["precision_sweep"] = precision_sweep(dbs_mask, dbs_target)
+        torch.cuda.empty_cache()
 
     if not args.no_psf:
         vec, dt, timing, acc_rate = measure("psf", args.psf_steps, max(args.warmup, 5))
         if rank == 0:
-            ps = pass_table(timing, abytes)
+            ps = pass_table(timing, abytes, {"k_psf_commit": vec.timed_accepts})
             ev = ps.get("k_psf_eval")
             out["incremental_psf_mode"] = {
                 "value": round(B * world * args.psf_steps / dt, 2), "unit": "env-steps/s",
@@ -420,6 +525,8 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ev["achieved_GBs"] / HBM_PEAK_GBS, 4),
                     "kernel_avg_ms": round(ev["avg_ms"], 4)},
                 "passes": rounded(ps),
+                "passes_note": "k_psf_commit is charged for the accepted envs only (24 N^2 B each); its "
+                               "launch covers all envs but rejected ones return at once",
                 "note": "same env semantics; a flip adds +-h_g(shifted) to the touched plane's cached field "
                         "(linearity of the propagation), no FFT per step; reported separately per SURVEY 8d"}
         vec.close()

@@ -44,14 +44,64 @@ def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def gather_to_rank0(t: torch.Tensor) -> Optional[torch.Tensor]:
-    """Concatenate equal-shaped per-rank tensors on rank 0 (None elsewhere).
-
-    Uses all_gather (supported by both nccl and gloo for any dtype)."""
+    """Concatenate equal-shaped per-rank tensors on rank 0 (None elsewhere):
+    one dist.gather, so only rank 0 receives (RCCL send/recv to the root over
+    xGMI; gloo on CPU)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return t
-    parts: List[torch.Tensor] = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(parts, t.contiguous())
-    return torch.cat(parts) if dist.get_rank() == 0 else None
+    home = t.device
+    t = t.contiguous()
+    if dist.get_backend() == "gloo" and t.is_cuda:   # gloo's gather takes host tensors
+        t = t.cpu()
+    if dist.get_rank() == 0:
+        parts: List[torch.Tensor] = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.gather(t, gather_list=parts, dst=0)
+        return torch.cat(parts).to(home)
+    dist.gather(t, dst=0)
+    return None
+
+
+class StepMetricGather:
+    """Per-step env metrics gathered to rank 0 every ``every`` steps (SURVEY 8e:
+    "batch K steps per gather"): rows accumulate in a device buffer [every, B, 5]
+    and one dist.gather moves them, so the collective's latency is paid once per
+    ``every`` steps.  flush() returns rank 0's [world * every, B, 5] block (rank
+    r's rows at [r * every, (r + 1) * every)) or None elsewhere / when empty."""
+
+    def __init__(self, n_env: int, every: int = 1, device=None):
+        self.every = max(1, int(every))
+        self.buf = torch.zeros((self.every, n_env, 5), dtype=torch.float64, device=device)
+        self.n = 0
+        self.gathered: List[torch.Tensor] = []
+
+    def add(self, reward, psnr, accepted, terminated, truncated):
+        self.buf[self.n] = pack_step_metrics(reward, psnr, accepted, terminated, truncated)
+        self.n += 1
+        if self.n == self.every:
+            return self.flush()
+        return None
+
+    def flush(self) -> Optional[torch.Tensor]:
+        if self.n == 0:
+            return None
+        out = gather_to_rank0(self.buf[:self.n])
+        self.n = 0
+        if out is not None:
+            self.gathered.append(out)
+        return out
+
+
+def describe_world(device=None) -> List[List]:
+    """[rank, world, local_rank, backend] as every rank saw it, gathered to rank 0
+    (the bench prints it so a multi-GPU line is self-checking)."""
+    rank, world, local = env_rank_world()
+    backend = dist.get_backend() if dist.is_initialized() else "none"
+    row = torch.tensor([rank, world, local], dtype=torch.int64,
+                       device=device if backend == "nccl" else "cpu")
+    allr = gather_to_rank0(row.unsqueeze(0))
+    if allr is None:
+        return []
+    return [[int(a), int(b), int(c), backend] for a, b, c in allr.cpu().tolist()]
 
 
 def pack_step_metrics(reward: torch.Tensor, psnr: torch.Tensor, accepted: torch.Tensor,

@@ -36,9 +36,16 @@ def _worker(rank, world, port, out):
     hist = hd.allreduce_hist(torch.tensor([rank + 1, 2 * rank], dtype=torch.int64))
     mx = hd.max_over_ranks(float(rank) + 0.5)
     lo, hi = hd.shard_range(1024, rank, world)
+    # K-step batched gather: 5 steps, every 3 -> one full block + one flushed partial block
+    mg = hd.StepMetricGather(B, every=3)
+    for k in range(5):
+        mg.add(reward + k, psnr, acc, term, trunc)
+    mg.flush()
+    seen = hd.describe_world()
     hd.barrier()
     if rank == 0:
-        out.put((g.tolist(), hist.tolist(), mx, (lo, hi)))
+        blocks = [b.tolist() for b in mg.gathered]
+        out.put((g.tolist(), hist.tolist(), mx, (lo, hi), blocks, seen))
     else:
         assert g is None
         out.put(None)
@@ -57,7 +64,14 @@ def test_gloo_world2_gather_and_reduce():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    g, hist, mx, (lo, hi) = next(r for r in res if r is not None)
+    g, hist, mx, (lo, hi), blocks, seen = next(r for r in res if r is not None)
+    assert seen == [[0, 2, 0, "gloo"], [1, 2, 1, "gloo"]]
+    assert [len(b) for b in blocks] == [6, 4]                  # world * steps per gather
+    for b, steps in zip(blocks, ([0, 1, 2], [3, 4])):
+        for r in range(2):
+            for j, k in enumerate(steps):
+                row = b[r * len(steps) + j]                     # rank r's step k, 4 envs x 5 metrics
+                assert [e[0] for e in row] == [i + 100 * r + k for i in range(4)]
     assert len(g) == 8                       # 4 envs x 2 ranks, rank order
     assert g[0][0] == 0.0 and g[4][0] == 100.0 and g[5][1] == 11.0 and g[4][4] == 1.0
     assert hist == [3, 2] and mx == 1.5 and (lo, hi) == (0, 512)
