@@ -52,8 +52,12 @@ struct JobDesc {
 #ifndef HBX_PANEL_PAD
 #define HBX_PANEL_PAD 0
 #endif
-#ifndef HBX_PANEL_A   // rows per panel of A (0: one panel of N rows = column-major lines)
-#define HBX_PANEL_A 0
+#ifndef HBX_PANEL_A   // rows per panel of A (0: one panel of N rows = column-major lines; values
+                      // below the row pass's block height round up to it).  Panels of the
+                      // block height make every k_rowfwd store contiguous (tools/membw2.hip:
+                      // 0.69 ms for the 128-job A vs 1.19 ms as 64-B pieces of line-major A)
+                      // and cost k_col2's line reads nothing (2.54 vs 2.55 ms replayed)
+#define HBX_PANEL_A 8
 #endif
 #ifndef HBX_PANEL_B   // rows per panel of B
 #define HBX_PANEL_B 16

@@ -4,8 +4,10 @@
 // an optional single-pixel flip applied on the fly (env.py:164-172).  The
 // intermediates are organised by spectral LINE kx (the N values over y), so
 // the column pass streams whole lines and the two transposes a 2-D FFT needs
-// live in LDS tiles of the row passes.  A is stored column-major ([kx][y]);
-// B in panels of 16 rows ([y / 16][kx][y % 16], hbx_internal.hpp), which gives
+// live in LDS tiles of the row passes.  A is stored in panels of the row block
+// height ([y / 8][kx][y % 8] at N = 1024: every k_rowfwd row block writes one
+// contiguous 64-KB panel per plane pair); B in panels of 16 rows
+// ([y / 16][kx][y % 16], hbx_internal.hpp), which gives
 // the column pass 256-B pieces to write and the row inverse pass 128-B pieces
 // to read (measured: 1-2 % over column-major B; 8-row panels made the column
 // pass's scattered 64-B writes cost 1 ms).
@@ -13,7 +15,7 @@
 //   k_rowfwd  GPB rows of a plane pair per block: bits -> one complex FFT per
 //             row pair (plane a real, plane b imaginary) -> Hermitian split ->
 //             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0) ->
-//             LDS tile transpose -> A[kx][y0..y0+GPB)       [HBM: read N^2/8 B, write 4 N^2 B per plane]
+//             LDS tile transpose -> A panel y0 / GPB       [HBM: read N^2/8 B, write 4 N^2 B per plane]
 //   k_col2    one lane group per half-spectrum line kx: FFT over y -> x H and
 //             x conj H (H is even in fx and ky) -> two IFFTs -> B lines kx
 //             and N - kx (N/2 for kx = 0); buffer loads / stores with one
@@ -77,6 +79,21 @@ using LayoutB = PanelLine<R, R * R, pan_b(R)>;
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
+// Row blocks per k_rowfwd workgroup (HBX_ROWFWD_ITER): a workgroup walks RIT
+// consecutive row blocks of one plane pair, so the stores of block i stay in
+// flight under the bit loads and row FFTs of block i + 1 (the next rows' mask
+// words are prefetched before the stores are issued: vmcnt counts loads and
+// stores in order, so waiting for them never waits for the stores).  With one
+// row block per workgroup the load -> FFT -> LDS tile -> store chain of the
+// two co-resident workgroups ran nearly serial.
+#ifndef HBX_ROWFWD_ITER
+#define HBX_ROWFWD_ITER 4
+#endif
+template <int R>
+constexpr int rowfwd_iters() {
+  return (R == 32 && (R * R / (kRowNT<R> / R)) % HBX_ROWFWD_ITER == 0) ? HBX_ROWFWD_ITER : 1;
+}
+
 template <int R, int NT, int SK>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
                                                    const uint32_t* __restrict__ mask,
@@ -84,9 +101,10 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int CH, float va, float vb) {
   constexpr int N = R * R;
-  constexpr int GPB = NT / R;          // rows per block
+  constexpr int GPB = NT / R;          // rows per row block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
   constexpr int SCR = GPB * R * (R + 1);
+  constexpr int RIT = rowfwd_iters<R>();
   static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
   __shared__ float2 tw[N];
   __shared__ __attribute__((aligned(16))) float2 lds[SCR];
@@ -97,88 +115,101 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   const int t = threadIdx.x % R;
   const int lane_base = (threadIdx.x & 63) - t;
   constexpr int RB = N / GPB;
-  int bid = xcd_pair<RB>(blockIdx.x);
-  const int rb = bid % RB;
-  bid /= RB;
+  constexpr int RBW = RB / RIT;        // workgroups per plane pair
+  int bid = RIT == 1 ? xcd_pair<RB>(blockIdx.x) : (int)blockIdx.x;
+  const int rbw = bid % RBW;
+  bid /= RBW;
   const int q = bid % (P / 2);
   const int j = bid / (P / 2);
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;  // uniform per block
-  const int y0 = rb * GPB;
-  const int y = y0 + grp;
   const int pa = 2 * q, pb = 2 * q + 1;
-
-  const uint32_t* rowa = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR + (size_t)y * WPR;
-  const uint32_t* rowb = rowa + (size_t)N * WPR;
+  const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
   uint32_t wa[WPR], wb[WPR];
-  if constexpr (WPR % 4 == 0) {
+  auto load_row = [&](int y) {
+    const uint32_t* rowa = plane_a + (size_t)y * WPR;
+    const uint32_t* rowb = rowa + (size_t)N * WPR;
+    if constexpr (WPR % 4 == 0) {
 #pragma unroll
-    for (int i = 0; i < WPR / 4; ++i) {
-      const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
-      const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
-      wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
-      wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < WPR; ++i) { wa[i] = rowa[i]; wb[i] = rowb[i]; }
-  }
-  if (jb.flip_plane >= 0 && jb.flip_pix / N == y) {  // env.py:164 flip, on the fly
-    const int col = jb.flip_pix % N;
-    const uint32_t bit = 1u << (col & 31);
-#pragma unroll
-    for (int i = 0; i < WPR; ++i) {
-      if (i == (col >> 5)) {
-        if (jb.flip_plane == pa) wa[i] ^= bit;
-        if (jb.flip_plane == pb) wb[i] ^= bit;
+      for (int i = 0; i < WPR / 4; ++i) {
+        const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
+        const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
+        wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
+        wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
       }
-    }
-  }
-  pk2 v[R];
+    } else {
 #pragma unroll
-  for (int jj = 0; jj < R; ++jj) {
-    const int w = (R * jj) >> 5;
-    const int sh = ((R * jj) & 31) + t;
-    v[jj] = (pk2){fmaf(vb, (float)((wa[w] >> sh) & 1u), va), fmaf(vb, (float)((wb[w] >> sh) & 1u), va)};
-  }
+      for (int i = 0; i < WPR; ++i) { wa[i] = rowa[i]; wb[i] = rowb[i]; }
+    }
+  };
+  load_row(rbw * RIT * GPB + grp);
   __syncthreads();  // tw visible
-  fft_group<R, false>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
-  lds_barrier();    // every group is done with its scratch: reuse as the tile
 
-  // Hermitian split -> tile[plane][kx][row]
-  float2* tile = lds;
-  const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0
-#pragma unroll
-  for (int k2 = 0; k2 < R / 2; ++k2) {
-    const float2 z = from_pk(v[k2]);
-    const float2 m = mirror_conj<R>(v, k2, t, lane_base);
-    float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-    float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
-    if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
-      fa = make_float2(z.x, zny.x);
-      fb = make_float2(z.y, zny.y);
-    }
-    const int kx = t + R * k2;
-    tile[tile_pos<R, GPB>(kx, grp)] = fa;
-    tile[tile_pos<R, GPB>(N / 2 + kx, grp)] = fb;
-  }
-  lds_barrier();
-  // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
   constexpr size_t PLA = plane_a_elems(R);
   float2* base = ws_a + ((size_t)j * P + pa) * PLA;
-  constexpr int CHUNKS = N * GPB / 2;
-  static_assert(CHUNKS % NT == 0, "chunking");
+#pragma unroll 1
+  for (int it = 0; it < RIT; ++it) {
+    const int y0 = (rbw * RIT + it) * GPB;
+    const int y = y0 + grp;
+    if (jb.flip_plane >= 0 && jb.flip_pix / N == y) {  // env.py:164 flip, on the fly
+      const int col = jb.flip_pix % N;
+      const uint32_t bit = 1u << (col & 31);
 #pragma unroll
-  for (int i = 0; i < CHUNKS / NT; ++i) {
-    const int c = threadIdx.x + NT * i;
-    const int r2 = (c % (GPB / 2)) * 2;
-    const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
-    const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
-    const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
-    const int pl = line / (N / 2);
-    // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
-    st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),
-               make_float4(a.x, a.y, b.x, b.y));
+      for (int i = 0; i < WPR; ++i) {
+        if (i == (col >> 5)) {
+          if (jb.flip_plane == pa) wa[i] ^= bit;
+          if (jb.flip_plane == pb) wb[i] ^= bit;
+        }
+      }
+    }
+    pk2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const int w = (R * jj) >> 5;
+      const int sh = ((R * jj) & 31) + t;
+      v[jj] = (pk2){fmaf(vb, (float)((wa[w] >> sh) & 1u), va), fmaf(vb, (float)((wb[w] >> sh) & 1u), va)};
+    }
+    if constexpr (RIT > 1) {
+      // next rows' words (the last iteration re-reads its own row: no conditional load)
+      load_row(it + 1 < RIT ? y + GPB : y);
+      if (it > 0) lds_barrier();   // every group has read the previous tile: scratch reusable
+    }
+    fft_group<R, false>(v, t, PaddedScratch<R>{lds + grp * R * (R + 1)}, tw);
+    lds_barrier();    // every group is done with its scratch: reuse as the tile
+
+    // Hermitian split -> tile[plane][kx][row]
+    float2* tile = lds;
+    const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0
+#pragma unroll
+    for (int k2 = 0; k2 < R / 2; ++k2) {
+      const float2 z = from_pk(v[k2]);
+      const float2 m = mirror_conj<R>(v, k2, t, lane_base);
+      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
+      float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
+        fa = make_float2(z.x, zny.x);
+        fb = make_float2(z.y, zny.y);
+      }
+      const int kx = t + R * k2;
+      tile[tile_pos<R, GPB>(kx, grp)] = fa;
+      tile[tile_pos<R, GPB>(N / 2 + kx, grp)] = fb;
+    }
+    lds_barrier();
+    // store tile lines: A[pa|pb][kx][y0 .. y0+GPB), 16 B per thread per chunk
+    constexpr int CHUNKS = N * GPB / 2;
+    static_assert(CHUNKS % NT == 0, "chunking");
+#pragma unroll
+    for (int i = 0; i < CHUNKS / NT; ++i) {
+      const int c = threadIdx.x + NT * i;
+      const int r2 = (c % (GPB / 2)) * 2;
+      const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
+      const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
+      const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
+      const int pl = line / (N / 2);
+      // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
+      st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),
+                 make_float4(a.x, a.y, b.x, b.y));
+    }
   }
 }
 
@@ -216,8 +247,11 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
 #define COL2_CMUL(a, b) pk_cmul((a), to_pk(b))
 #define COL2_CMULC(a, b) from_pk(pk_cmulc((a), to_pk(b)))
 #endif
+#ifndef HBX_COL2_ITER
+#define HBX_COL2_ITER 4
+#endif
 template <int R>
-__host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
+__host__ __device__ constexpr int col2_iters() { return R == 32 ? HBX_COL2_ITER : (R == 16 ? 2 : 1); }
 
 template <int R, int SK>
 __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
@@ -619,7 +653,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if (e != hipSuccess) return e;
   } else {
   {
-    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R));
+    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
     if (tm) tm->begin(0, st);
     hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);

@@ -9,7 +9,7 @@ mkdir -p gpurun_out/variants
 for lib in $LIBS; do
   name=$(basename $lib .so)
   HBX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-psf --cpu-sample 0 --dbs-flips 0 --no-probe \
-      --no-psnr-check > gpurun_out/variants/$name.json 2> gpurun_out/variants/$name.err || exit 1
+      --no-psnr-check --no-precision --no-ppo > gpurun_out/variants/$name.json 2> gpurun_out/variants/$name.err || exit 1
   python -c "
 import json; d = json.load(open('gpurun_out/variants/$name.json'))
 print('%-48s %9.0f' % ('$name', d['value']), ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in d['passes'].items()))"
