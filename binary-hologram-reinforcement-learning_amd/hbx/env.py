@@ -28,6 +28,55 @@ RW = 800.0   # env.py:29
 
 OBS_KEYS = ("state_record", "state", "pre_model", "recon_image", "target_image")
 
+# SB3's VecEnv base class when stable-baselines3 is importable (train-PPO.py:296-322 hands the
+# env to PPO; optimize_hyperparameter.py:317-318 wraps it in VecNormalize), so isinstance checks
+# and VecEnvWrapper stacks see a VecEnv; otherwise the same method set, duck-typed.
+try:  # pragma: no cover - SB3 is absent in this image
+    from stable_baselines3.common.vec_env import VecEnv as _VecEnvBase
+    HAVE_SB3 = True
+except Exception:  # noqa: BLE001
+    _VecEnvBase = object
+    HAVE_SB3 = False
+
+# per-env attributes of the reference env (env.py:65-81) readable through get_attr
+_STATE_ATTRS = {"initial_psnr": "init_psnr", "previous_psnr": "prev_psnr", "max_psnr_diff": "max_psnr_diff",
+                "steps": "steps", "flip_count": "flip_count", "psnr_sustained_steps": "sustained"}
+# EnvParams fields settable through set_attr (shared by every env of the batch)
+_PARAM_ATTRS = {"max_steps": ("max_steps", int), "T_PSNR": ("t_psnr", float), "T_steps": ("t_steps", int),
+                "T_PSNR_DIFF": ("t_psnr_diff", float)}
+
+
+class LazyObs(dict):
+    """Dict observation kept on the GPU whose values become numpy arrays on first
+    access (cached): an SB3 rollout buffer that reads every key pays one device ->
+    host copy per key, a consumer that reads none pays nothing.  ``.device(key)``
+    returns the device tensor without a copy."""
+
+    def __init__(self, tensors: dict):
+        super().__init__()
+        self._t = dict(tensors)
+        for k in self._t:
+            dict.__setitem__(self, k, None)
+
+    def __getitem__(self, k):
+        v = dict.__getitem__(self, k)
+        if v is None:
+            v = self._t[k].detach().cpu().numpy()
+            dict.__setitem__(self, k, v)
+        return v
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def device(self, k):
+        return self._t[k]
+
 
 class EnvState:
     """Device buffers of B environments (env.py:65-81 attributes)."""
@@ -80,8 +129,17 @@ class EnvState:
             raise ValueError("action out of range [0, CH*H*W) passed to step()")
 
 
-class HologramVecEnv:
-    """B environments on one GPU, stepped together (SB3 VecEnv-style API).
+class HologramVecEnv(_VecEnvBase):
+    """B environments on one GPU, stepped together -- an SB3 VecEnv (subclass of
+    stable_baselines3's VecEnv when it is importable, the same method set otherwise:
+    reset, step_async / step_wait / step, get_attr, set_attr, env_method,
+    env_is_wrapped, seed, get_images, render, close).
+
+    obs_format: "torch" (default: device tensors, the batched kernels' own
+    output), "numpy" (numpy arrays, what SB3's rollout buffers assign from) or
+    "lazy" (LazyObs: device tensors turned into numpy on first access).  With the
+    numpy formats rewards come back float32 and terminal observations numpy, as
+    SB3's DummyVecEnv returns them.
 
     target_source(i) -> target tensor [G, H, W] (or [1, G, H, W]) in [0, 1]
     pre_model_fn(target[1, G, H, W]) -> pre-model output [1, CH, H, W] in [0, 1]
@@ -110,7 +168,7 @@ class HologramVecEnv:
                  device: Optional[int] = None, pre_model_source: Optional[Callable] = None,
                  mode: str = "fft", refresh_every: int = 2048, reward: str = "psnr",
                  importance_samples: int = 10000, importance_seed: int = 0,
-                 action_format: str = "discrete"):
+                 action_format: str = "discrete", obs_format: str = "torch"):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
         if mode not in ("fft", "psf"):
@@ -118,6 +176,9 @@ class HologramVecEnv:
         if mode == "psf" and "recon_image" in obs_keys:
             raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
                              "drop it from obs_keys or use mode='fft'")
+        if obs_format not in ("torch", "numpy", "lazy"):
+            raise ValueError(f"obs_format must be 'torch', 'numpy' or 'lazy', got {obs_format!r}")
+        self.obs_format = obs_format
         if action_format not in ("discrete", "multidiscrete"):
             raise ValueError(f"action_format must be 'discrete' or 'multidiscrete', got {action_format!r}")
         self.action_format = action_format
@@ -183,6 +244,14 @@ class HologramVecEnv:
         self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
         self.episode_count = 0
+        if HAVE_SB3:  # pragma: no cover - SB3 absent here
+            _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
+        else:
+            self.render_mode = None
+            self.reset_infos = [{} for _ in range(self.num_envs)]
+            self._seeds = [None for _ in range(self.num_envs)]
+            self._options = [{} for _ in range(self.num_envs)]
+        self.metadata = {"render_modes": []}
 
     # -- reset -------------------------------------------------------------------
     def _load_env(self, i: int):
@@ -228,10 +297,22 @@ class HologramVecEnv:
             st.t_psnr_diff[i] = tpd
 
     def reset(self, seed=None, options=None):
+        """VecEnv.reset: every env; returns the batched observation (obs_format).
+        Seeds given through seed() are recorded and consumed here (the reference
+        ignores reset's seed, env.py:90 -- SURVEY F9)."""
         self.reset_envs(range(self.num_envs))
         if self._ginten is not None and self.state.intensity is not None:
             self._ginten.zero_()
-        return self.observe(stepped=False)
+        self._seeds = [None for _ in range(self.num_envs)]
+        self.reset_infos = [{} for _ in range(self.num_envs)]
+        return self._format(self.observe(stepped=False))
+
+    def _format(self, obs: dict):
+        if self.obs_format == "numpy":
+            return _to_numpy(obs)
+        if self.obs_format == "lazy":
+            return LazyObs(obs)
+        return obs
 
     # -- step --------------------------------------------------------------------
     def step_async(self, actions):
@@ -275,11 +356,14 @@ class HologramVecEnv:
             self._since_refresh = 0
 
     def step(self, actions):
-        """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset."""
+        """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
+        (done envs report their last observation as info["terminal_observation"])."""
         reward, psnr, acc, term, trunc = self.step_device(actions)
         self.state.check_error()
         obs = self.observe(stepped=True)
         r = reward.cpu().numpy()
+        if self.obs_format != "torch":
+            r = r.astype(np.float32)
         t = term.cpu().numpy().astype(bool)
         tr = trunc.cpu().numpy().astype(bool)
         dones = t | tr
@@ -287,12 +371,95 @@ class HologramVecEnv:
         if self.auto_reset and dones.any():
             done_ids = np.nonzero(dones)[0].tolist()
             term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}
+            if self.obs_format != "torch":
+                term_obs = _to_numpy(term_obs)
             for j, i in enumerate(done_ids):
                 infos[i]["terminal_observation"] = {k: v[j] for k, v in term_obs.items()}
                 infos[i]["TimeLimit.truncated"] = bool(tr[i] and not t[i])
             self.reset_envs(done_ids)
             obs = self.observe(stepped=False)
-        return obs, r, dones, infos
+        return self._format(obs), r, dones, infos
+
+    # -- SB3 VecEnv surface (stable_baselines3/common/vec_env/base_vec_env.py) ---------
+    def _indices(self, indices):
+        if indices is None:
+            return list(range(self.num_envs))
+        if isinstance(indices, (int, np.integer)):
+            return [int(indices)]
+        return [int(i) for i in indices]
+
+    def get_attr(self, attr_name: str, indices=None):
+        """Per-env values of the reference env's attributes (env.py:65-81:
+        initial_psnr, previous_psnr, steps, flip_count, psnr_sustained_steps,
+        max_psnr_diff) or this object's attribute, once per requested env."""
+        idx = self._indices(indices)
+        if attr_name in _STATE_ATTRS:
+            vals = getattr(self.state, _STATE_ATTRS[attr_name]).cpu().tolist()
+            return [vals[i] for i in idx]
+        if attr_name in _PARAM_ATTRS:
+            v = getattr(self.params, _PARAM_ATTRS[attr_name][0])
+            return [v for _ in idx]
+        v = getattr(self, attr_name)
+        return [v for _ in idx]
+
+    def set_attr(self, attr_name: str, value, indices=None):
+        """max_steps / T_PSNR / T_steps / T_PSNR_DIFF (env.py:38) go to the
+        batch's shared EnvParams and so must be set for every env at once; other
+        names set this object's attribute."""
+        idx = self._indices(indices)
+        if attr_name in _PARAM_ATTRS:
+            if sorted(idx) != list(range(self.num_envs)):
+                raise ValueError(f"{attr_name} is shared by the whole batch: set it for every env (indices=None)")
+            field, cast = _PARAM_ATTRS[attr_name]
+            setattr(self.params, field, cast(value))
+            return
+        if attr_name in _STATE_ATTRS:
+            raise AttributeError(f"{attr_name} is env state; it changes only through reset / step")
+        setattr(self, attr_name, value)
+
+    def env_method(self, method_name: str, *method_args, indices=None, **method_kwargs):
+        """Methods of the individual envs: reset (those envs; returns their
+        observations), render / get_images (None per env), or a method of this
+        object called once per requested env."""
+        idx = self._indices(indices)
+        if method_name == "reset":
+            self.reset_envs(idx)
+            obs = self.observe(stepped=False)
+            if self.obs_format != "torch":
+                obs = _to_numpy(obs)
+            return [{k: v[i] for k, v in obs.items()} for i in idx]
+        if method_name in ("render", "get_images"):
+            return [None for _ in idx]
+        fn = getattr(self, method_name)
+        return [fn(*method_args, **method_kwargs) for _ in idx]
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False for _ in self._indices(indices)]
+
+    def seed(self, seed=None):
+        """Record seed + i for env i (consumed at the next reset, as SB3 >= 2 does);
+        the simulation itself draws nothing at random."""
+        if seed is None:
+            seed = int(np.random.default_rng().integers(0, 2 ** 31 - 1))
+        self._seeds = [int(seed) + i for i in range(self.num_envs)]
+        return list(self._seeds)
+
+    def set_options(self, options=None):
+        opts = options if isinstance(options, list) else [options or {}] * self.num_envs
+        self._options = [dict(o or {}) for o in opts]
+
+    def get_images(self):
+        return [None for _ in range(self.num_envs)]
+
+    def render(self, mode=None):
+        return None
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def getattr_depth_check(self, name, already_found):
+        return self if hasattr(self, name) and already_found else None
 
     # -- observations (env.py:135-140,176-181) ----------------------------------------
     def observe(self, stepped: bool):
