@@ -105,6 +105,12 @@ def main():
             info["frac_wait_any"] = mean("SQ_WAIT_ANY") / wc if mean("SQ_WAIT_ANY") else None
             info["frac_wait_inst"] = mean("SQ_WAIT_INST_ANY") / wc if mean("SQ_WAIT_INST_ANY") else None
             info["frac_active"] = mean("SQ_ACTIVE_INST_ANY") / wc if mean("SQ_ACTIVE_INST_ANY") else None
+        if k == "k_psf_commit":
+            # only accepted envs rewrite their plane: the per-launch algorithmic bytes depend on
+            # the accept count (bench.py charges the accepted jobs); the PMC bytes are the truth here
+            info["alg_bytes_per_launch"] = None
+            info["alg_GBs"] = None
+            info["note"] = "24 N^2 B per ACCEPTED job; see hbm_bytes_per_launch / bench.py passes"
         res["kernels"][k] = info
     txt = json.dumps(res, indent=1)
     print(txt)
