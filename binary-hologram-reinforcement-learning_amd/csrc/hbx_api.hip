@@ -64,6 +64,8 @@ struct hbx_plan {
   float2* map_y = nullptr;       // [P + P/2 + 1][N][N]
   double* walk_partial = nullptr;  // [kWalkMaxK x blocks][2] (lazy, hbx_dbs_walk_psf)
   size_t walk_partial_elems = 0;
+  int* walk_counter = nullptr;     // fused walk step: arrival tickets [9] (zero between launches)
+  int walk_split = 0;              // HBX_WALK_SPLIT=1: three-launch batches for every K
 };
 
 namespace {
@@ -189,6 +191,10 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
     const char* ev = std::getenv("HBX_COLBITS");
     pd.colbits = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
   }
+  {
+    const char* ev = std::getenv("HBX_WALK_SPLIT");   // A/B switch: the v5 three-launch walk batches
+    p->walk_split = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
+  }
   const size_t hrow = (size_t)(N / 2 + 1) * N;
   std::vector<float2> ht((size_t)G * hrow);
   const double scale = 1.0 / ((double)N * (double)N);  // ifft2 normalisation
@@ -255,6 +261,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->pd.hpsf) (void)hipFree(p->pd.hpsf);
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
   if (p->walk_partial) (void)hipFree(p->walk_partial);
+  if (p->walk_counter) (void)hipFree(p->walk_counter);
   if (p->pd.psf_order) (void)hipFree(p->pd.psf_order);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
@@ -344,6 +351,7 @@ int ensure_hpsf(hbx_plan_t p, hipStream_t st) {
   amp.va = 0.0f;
   amp.vb = 1.0f;
   amp.timer = nullptr;
+  amp.store_kind = HBX_PRECISION_F32;   // h is a table of the product path, whatever the plan's precision
   hipError_t e = hbx::launch_jobs_full(nullptr, 1, G, p->jobs, st);
   if (e == hipSuccess)
     e = hbx::run_jobs(amp, p->jobs, G, reinterpret_cast<const uint32_t*>(mask), target, nullptr, field, st);
@@ -804,9 +812,13 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   const PlanDev& pd = p->pd;
   // sized once for every K, so the buffer never moves: launches captured into a
   // graph (one per K) stay valid
-  size_t need = 0;
+  size_t need = (size_t)hbx::walk_step_blocks(pd.N) * hbx::kWalkStepMaxTerms;
   for (int k = 1; k <= hbx::kWalkMaxK; ++k)
     need = std::max(need, (size_t)k * hbx::walk_blocks_per_job(pd.N, k) * 2);
+  if (!p->walk_counter) {   // allocation: first call only, outside capture
+    if (hipMalloc(&p->walk_counter, hbx::kWalkScratchBytes) != hipSuccess) return fail(HBX_ERR_NOMEM, "walk scratch");
+    if (hipMemset(p->walk_counter, 0, hbx::kWalkScratchBytes) != hipSuccess) return fail(HBX_ERR_HIP, "walk scratch");
+  }
   if (need > p->walk_partial_elems) {   // allocation: first call only, outside capture
     if (p->walk_partial) (void)hipFree(p->walk_partial);
     p->walk_partial = nullptr;
@@ -828,11 +840,16 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   l.log_psnr = accept_psnr;
   l.log_cap = accept_cap;
   l.partial = p->walk_partial;
+  l.counter = p->walk_counter;
+  l.fused = p->walk_split ? 0 : 1;
   l.K = K;
   l.batches = batches;
   l.count = pixel_count(p);
   l.peak = p->optics.peak;
   l.rel = p->optics.rel_scale;
+  // the decoded next actions a previous launch left are keyed on (position, order
+  // pointer); a new call may bring new order contents at the same address: invalidate
+  HBX_HIP(hipMemsetAsync(p->walk_counter + hbx::kWalkCounters, 0xff, sizeof(int64_t), st));
   HBX_HIP(hbx::launch_walk(pd, l, st));
   return HBX_OK;
 }

@@ -219,13 +219,34 @@ struct WalkLaunch {
   int64_t* log_pos;
   double* log_psnr;
   int64_t log_cap;
-  double* partial;   // [K][walk_blocks_per_job(N, K)][2]
+  double* partial;   // split batch: [K][walk_blocks_per_job(N, K)][2]; fused step: [blocks][terms]
+  int* counter;      // fused step: walk scratch (kWalkScratchBytes): tickets, then WalkPre
+  int fused;         // 1: one k_walk_step launch per batch when K has a fused variant
   int K, batches;
   double count, peak;
   int rel;
 };
 constexpr int kWalkMaxK = 256;
 int walk_blocks_per_job(int N, int K);
+int walk_step_blocks(int N);
+bool walk_fused_k(int K);
+constexpr int kWalkStepMaxTerms = 26;   // 2 K + 3 K (K-1) / 2 at K = 4: max over the fused variants
+// fused-step scratch: int counters [kWalkCounters] (arrival tickets [0, kWalkTickets),
+// zero between launches), then the WalkPre the deciding block leaves for the next launch
+constexpr int kWalkCounters = 16;
+constexpr int kWalkTickets = 9;
+constexpr int kWalkPreMax = 4;          // the largest fused K
+struct WalkPre {
+  int64_t pos;              // valid for this walk position (-1: invalid; cleared per API call)
+  const int64_t* order;     //   and this order array
+  int32_t n;                // actions filled
+  int32_t pad;
+  int32_t ch[kWalkPreMax];   // order[pos + j] decoded: channel (-1: not a valid action) ...
+  int32_t pix[kWalkPreMax];  //   ... and pixel
+  float delta[kWalkPreMax];  // vb (1 - 2 bit) of each action's pixel before its flip
+  float cdelta[2];           // the pending commits' vb (2 bit - 1) after their flips
+};
+constexpr size_t kWalkScratchBytes = kWalkCounters * sizeof(int) + sizeof(WalkPre);
 hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st);
 hipError_t launch_psf_commit(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                              float2* field, float* inten, const int32_t* accept_flag, hipStream_t st);

@@ -84,6 +84,7 @@ struct WalkArgs {
   float vb;
   double count, peak;
   int rel;
+  int commit_only;           // fused step: apply the pending commits, evaluate nothing
 };
 
 __global__ __launch_bounds__(kWalkNT) void k_walk_eval(WalkArgs a) {
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
   // one snapshot of the state (uniform scalar loads, one round trip)
   const hbx_dbs_walk_t ws = *w;
   if (ws.done || ws.halt) {
-    if (threadIdx.x == 0) w->commit_ch = -1;
+    if (threadIdx.x == 0) w->split_ch1 = 0;
     return;
   }
   const int64_t pos = ws.pos, total = ws.total < a.n_order ? ws.total : a.n_order;
@@ -240,8 +241,8 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
     const int64_t n = ws.accepted;
     if (n < a.log_cap) { a.log_pos[n] = pos + acc; a.log_psnr[n] = ps; }
     nw.accepted = n + 1;
-    nw.commit_ch = ch;
-    nw.commit_pix = pix;
+    nw.split_ch1 = ch + 1;
+    nw.split_pix = pix;
     nw.pos = pos + acc + 1;
     if (ws.stop_enabled && ps - ws.init_psnr >= ws.stop_diff) {   // DBS_ratio_0.5.py:366-372
       nw.done = 1;
@@ -250,7 +251,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
     if (ws.refresh_every > 0 && (n + 1) % ws.refresh_every == 0) nw.halt = 1;
   } else {
     if (kv > 0) nw.last_psnr = s_ps[kv - 1];
-    nw.commit_ch = -1;
+    nw.split_ch1 = 0;
     nw.pos = pos + kv;
   }
   if (nw.pos >= total) nw.done = 1;
@@ -261,9 +262,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_decide(WalkArgs a) {
 // I_g += (|U_c'|^2 - |U_c|^2) / P
 __global__ __launch_bounds__(kWalkNT) void k_walk_commit(WalkArgs a) {
   hbx_dbs_walk_t* w = a.w;
-  const int ch = w->commit_ch;
+  const int ch = w->split_ch1 - 1;
   if (ch < 0) return;
-  const int pix = w->commit_pix;
+  const int pix = w->split_pix;
   const int N = a.N, P = a.P;
   const size_t hw = (size_t)N * N;
   const int g = ch / P, r = pix / N, col = pix % N;
@@ -297,6 +298,585 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_commit(WalkArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused walk step (ABI v7): ONE launch per batch.
+//
+//   1. every block applies the previous batch's accepted flip(s) to its pixel
+//      slice of the plane field(s) and group intensity(ies) (the split walk's
+//      k_walk_commit), keeping the updated values in registers;
+//   2. the same block evaluates the batch's K candidates on that slice against
+//      the updated state: per candidate the increments sum dI T, sum (2I+dI) dI,
+//      and -- TWO = true -- for every candidate pair (i, j) of one colour group
+//      sum dI_i dI_j, plus, for a pair in one plane, the field cross term
+//      X = 2 d_i d_j Re(h_i conj h_j) / P through sum X T, sum (2I + 2dI_i +
+//      2dI_j + X) X (the exact change of sum I T / sum I^2 when BOTH flips are
+//      applied: I' = I + dI_i + dI_j + X);
+//   3. block partials go out as write-through (sc1) stores, each block then
+//      takes a ticket on one agent-scope counter after its stores have drained;
+//      the block holding the last ticket reads every partial with sc1 loads
+//      (MI355X_MICROARCH.md, inter-workgroup hand-off row 1: no release fence)
+//      and decides: the first candidate that strictly improves the PSNR
+//      (DBS_1024_24.py:355), and -- TWO -- the first one after it that improves
+//      on the state WITH it (pairwise terms), i.e. up to two accepts of the
+//      serial loop per batch; the batch ends after the second accept.  It
+//      toggles the mask bits, updates the group sums, the accept log and the
+//      walk state, and leaves the accepted flips as the next launch's commits.
+//
+// A batch then costs one kernel boundary instead of three, and at acceptance
+// ~0.5 visits ~3.2 candidates (K = 4, two accepts) instead of ~1.6.  Commits
+// left pending when the walk is done or halted are applied by the next launch
+// (it finds no candidates and only commits); the host issues one after the
+// walk ends and drops them when it re-propagates exactly (the mask already
+// holds every accepted flip).
+#ifndef HBX_WALK_STEP_BLOCKS
+#define HBX_WALK_STEP_BLOCKS 256
+#endif
+constexpr int kWalkStepBlocksMax = HBX_WALK_STEP_BLOCKS;
+constexpr int kSc1 = 16;   // buffer cache policy bit sc1 (gfx950): write-through stores, L2-fresh loads
+typedef unsigned int walk_u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), (short)0, (int)bytes,
+                                           0x00020000);
+}
+
+// fixed-order block sum of NT per-thread values into out (LDS): every thread's
+// values go to LDS once, then 8 lanes per term sum 32 each and one lane per term
+// the 8 (a shuffle tree per term costs ~4 us at NT = 26)
+template <int NT>
+__device__ __forceinline__ void block_sum_lds(const double (&v)[NT], double (*all)[kWalkNT], double (*seg)[8],
+                                              double* out) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) all[t][threadIdx.x] = v[t];
+  __syncthreads();
+  if ((int)threadIdx.x < NT * 8) {
+    const int t = threadIdx.x / 8, sg = threadIdx.x % 8;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < kWalkNT / 8; ++i) acc += all[t][sg + 8 * i];
+    seg[t][sg] = acc;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < NT) {
+    double acc = 0.0;
+#pragma unroll
+    for (int sg = 0; sg < 8; ++sg) acc += seg[threadIdx.x][sg];
+    out[threadIdx.x] = acc;
+  }
+  __syncthreads();
+}
+
+struct WalkCand {
+  int ch, pix, g, r, col;
+  float delta;
+  bool ok;
+};
+
+
+template <int K, bool TWO>
+__global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restrict__ counter) {
+  constexpr int NP = TWO ? K * (K - 1) / 2 : 0;
+  constexpr int NT = 2 * K + 3 * NP;
+  constexpr int NG = HBX_MAX_GROUPS;
+  static_assert(K <= kWalkPreMax, "fused K");
+  __shared__ double red_all[NT][kWalkNT];
+  __shared__ double red_seg[NT][8];
+  __shared__ double tot[NT];
+  __shared__ double s_ps[K + NP];
+  __shared__ int s_nch[2 * kWalkPreMax], s_npix[2 * kWalkPreMax];
+  __shared__ uint64_t s_nwd[2 * kWalkPreMax];
+  __shared__ int s_last;
+  __shared__ WalkCand s_cd[K];           // the decider's candidates, indexed at run time
+  hbx_dbs_walk_t* w = a.w;
+  WalkPre* prep = reinterpret_cast<WalkPre*>(counter + kWalkCounters);
+#ifdef HBX_WALK_TIMING
+  uint64_t tt[12];
+  tt[0] = __builtin_amdgcn_s_memrealtime();
+#define HBX_TT(i) tt[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define HBX_TT(i)
+#endif
+  // the state the previous launch left, and its decider's decoded next actions: one
+  // round trip, by one wave per block (48 lanes, a word each) through LDS -- when every
+  // wave of the grid loaded the same two lines itself, the K = 1, 2, 4 variants
+  // measured 2-27 us (mean 7.5) before the first block could start streaming
+  static_assert(sizeof(hbx_dbs_walk_t) % 4 == 0 && sizeof(WalkPre) % 4 == 0, "word copies");
+  constexpr int kWsWords = (int)(sizeof(hbx_dbs_walk_t) / 4), kPreWords = (int)(sizeof(WalkPre) / 4);
+  static_assert(kWsWords + kPreWords <= 64, "one wave");
+  __shared__ hbx_dbs_walk_t s_ws;
+  __shared__ WalkPre s_pre;
+  if ((int)threadIdx.x < kWsWords)
+    reinterpret_cast<int*>(&s_ws)[threadIdx.x] = reinterpret_cast<const int*>(w)[threadIdx.x];
+  else if ((int)threadIdx.x < kWsWords + kPreWords)
+    reinterpret_cast<int*>(&s_pre)[threadIdx.x - kWsWords] = reinterpret_cast<const int*>(prep)[threadIdx.x - kWsWords];
+  __syncthreads();
+  const hbx_dbs_walk_t ws = s_ws;
+  const WalkPre pre = s_pre;
+  const int N = a.N, P = a.P, G = a.G, CH = G * P;
+  const size_t hw = (size_t)N * N;
+  const float invp = 1.0f / (float)P;
+  const int cch[2] = {ws.commit_ch, ws.commit2_ch1 - 1};
+  const int cpx[2] = {ws.commit_pix, ws.commit_pix2};
+  const int nc = cch[0] < 0 ? 0 : (cch[1] < 0 ? 1 : 2);
+  const int64_t total = ws.total < a.n_order ? ws.total : a.n_order;
+  const int64_t pos = ws.pos;
+  const int64_t left = (!a.commit_only && !ws.done && !ws.halt && total > pos) ? total - pos : 0;
+  const int kcap = a.K < K ? a.K : K;     // a launch may run a wider variant
+  const int kv = (int)(left < (int64_t)kcap ? left : (int64_t)kcap);
+  if (nc == 0 && kv == 0) return;        // uniform over the grid
+  HBX_TT(8);
+  const bool use_pre = pre.pos == pos && pre.order == a.order && pre.n >= kv;
+  // the actions that can follow this batch, order[pos + 1 .. pos + kv + 3]: loaded now
+  // (only the deciding block uses them, for the next launch's WalkPre)
+  const int64_t n_next = total - pos - 1;
+  const int nn = (int)(n_next < (int64_t)(kv + kWalkPreMax - 1) ? (n_next > 0 ? n_next : 0) : kv + kWalkPreMax - 1);
+  int64_t nact = -1;
+  if ((int)threadIdx.x < nn) nact = a.order[pos + 1 + threadIdx.x];
+
+  WalkCand cm[2], cd[K];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    cm[c].ok = c < nc;
+    const int ch = cm[c].ok ? cch[c] : 0, pix = cm[c].ok ? cpx[c] : 0;
+    cm[c].ch = ch; cm[c].pix = pix; cm[c].g = ch / P; cm[c].r = pix / N; cm[c].col = pix % N;
+    if (use_pre) {
+      cm[c].delta = pre.cdelta[c];
+    } else {
+      const uint64_t wd = a.mask[((size_t)ch * N + cm[c].r) * (N / 64) + cm[c].col / 64];
+      cm[c].delta = a.vb * (float)(2 * (int)((wd >> (cm[c].col & 63)) & 1ull) - 1);   // after the flip
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    int ch = 0, pix = 0;
+    if (use_pre) {
+      cd[j].ok = j < kv && pre.ch[j] >= 0;
+      ch = cd[j].ok ? pre.ch[j] : 0;
+      pix = cd[j].ok ? pre.pix[j] : 0;
+    } else {
+      const int64_t act = j < kv ? a.order[pos + j] : -1;
+      cd[j].ok = act >= 0 && act < (int64_t)CH * (int64_t)hw;
+      ch = cd[j].ok ? (int)(act / (int64_t)hw) : 0;
+      pix = cd[j].ok ? (int)(act % (int64_t)hw) : 0;
+    }
+    cd[j].ch = ch; cd[j].pix = pix; cd[j].g = ch / P; cd[j].r = pix / N; cd[j].col = pix % N;
+    if (use_pre) {
+      cd[j].delta = pre.delta[j];
+    } else {
+      const uint64_t wd = a.mask[((size_t)ch * N + cd[j].r) * (N / 64) + cd[j].col / 64];
+      cd[j].delta = a.vb * (float)(1 - 2 * (int)((wd >> (cd[j].col & 63)) & 1ull));   // before the flip
+    }
+  }
+  HBX_TT(1);
+
+  double acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = 0.0;
+  const int nq = (int)(hw / 4);
+  // per quad: every load (pending commits, then each candidate's plane / intensity /
+  // target / shifted single-pixel field) is issued before any arithmetic or store, so a
+  // quad costs one memory round trip; values a commit produces replace the loaded ones
+  for (int q = blockIdx.x * kWalkNT + threadIdx.x; q < nq; q += gridDim.x * kWalkNT) {
+    const int y = (4 * q) / N, x0 = (4 * q) % N;
+    float cu[2][8], ci[2][4], chh[2][8];
+    float lu[K][8], li[K][4], lt[K][4], lh[K][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c >= nc) break;
+      const float4* U = reinterpret_cast<const float4*>(a.field + (size_t)cm[c].ch * hw);
+      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+      cu[c][0] = u01.x; cu[c][1] = u01.y; cu[c][2] = u01.z; cu[c][3] = u01.w;
+      cu[c][4] = u23.x; cu[c][5] = u23.y; cu[c][6] = u23.z; cu[c][7] = u23.w;
+      const float4 iv = reinterpret_cast<const float4*>(a.inten + (size_t)cm[c].g * hw)[q];
+      ci[c][0] = iv.x; ci[c][1] = iv.y; ci[c][2] = iv.z; ci[c][3] = iv.w;
+      const float2* hrow = a.hpsf + (size_t)cm[c].g * hw + (size_t)wfold(y - cm[c].r, N) * N;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float2 hv = hrow[wfold(x0 + k - cm[c].col, N)];
+        chh[c][2 * k] = hv.x;
+        chh[c][2 * k + 1] = hv.y;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j >= kv || !cd[j].ok) continue;
+      const float4* U = reinterpret_cast<const float4*>(a.field + (size_t)cd[j].ch * hw);
+      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+      lu[j][0] = u01.x; lu[j][1] = u01.y; lu[j][2] = u01.z; lu[j][3] = u01.w;
+      lu[j][4] = u23.x; lu[j][5] = u23.y; lu[j][6] = u23.z; lu[j][7] = u23.w;
+      const float4 iv = reinterpret_cast<const float4*>(a.inten + (size_t)cd[j].g * hw)[q];
+      li[j][0] = iv.x; li[j][1] = iv.y; li[j][2] = iv.z; li[j][3] = iv.w;
+      const float4 tv = reinterpret_cast<const float4*>(a.target + (size_t)cd[j].g * hw)[q];
+      lt[j][0] = tv.x; lt[j][1] = tv.y; lt[j][2] = tv.z; lt[j][3] = tv.w;
+      const float2* hrow = a.hpsf + (size_t)cd[j].g * hw + (size_t)wfold(y - cd[j].r, N) * N;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float2 hv = hrow[wfold(x0 + k - cd[j].col, N)];
+        lh[j][2 * k] = hv.x;
+        lh[j][2 * k + 1] = hv.y;
+      }
+    }
+    // commits (the second applies on top of the first when they share a plane / group)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c >= nc) break;
+      if (c == 1 && cm[1].ch == cm[0].ch) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cu[1][e] = cu[0][e];
+      }
+      if (c == 1 && cm[1].g == cm[0].g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ci[1][e] = ci[0][e];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float ur = cu[c][2 * k], ui = cu[c][2 * k + 1];
+        ci[c][k] += flip_dI(ur, ui, chh[c][2 * k], chh[c][2 * k + 1], cm[c].delta, invp);
+        cu[c][2 * k] = fmaf(cm[c].delta, chh[c][2 * k], ur);
+        cu[c][2 * k + 1] = fmaf(cm[c].delta, chh[c][2 * k + 1], ui);
+      }
+      float4* U = reinterpret_cast<float4*>(a.field + (size_t)cm[c].ch * hw);
+      U[2 * q] = make_float4(cu[c][0], cu[c][1], cu[c][2], cu[c][3]);
+      U[2 * q + 1] = make_float4(cu[c][4], cu[c][5], cu[c][6], cu[c][7]);
+      reinterpret_cast<float4*>(a.inten + (size_t)cm[c].g * hw)[q] = make_float4(ci[c][0], ci[c][1], ci[c][2], ci[c][3]);
+    }
+    float dI[K][4];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (j >= kv || !cd[j].ok) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dI[j][k] = 0.0f;
+        continue;
+      }
+      // the state after the pending commits: their planes / intensities replace the loads
+      if (nc > 1 && cd[j].ch == cm[1].ch) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) lu[j][e] = cu[1][e];
+      } else if (nc > 0 && cd[j].ch == cm[0].ch) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) lu[j][e] = cu[0][e];
+      }
+      if (nc > 1 && cd[j].g == cm[1].g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) li[j][e] = ci[1][e];
+      } else if (nc > 0 && cd[j].g == cm[0].g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) li[j][e] = ci[0][e];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d = flip_dI(lu[j][2 * k], lu[j][2 * k + 1], lh[j][2 * k], lh[j][2 * k + 1], cd[j].delta, invp);
+        dI[j][k] = d;
+        acc[j] = fma((double)d, (double)lt[j][k], acc[j]);
+        acc[K + j] = fma((double)fmaf(2.0f, li[j][k], d), (double)d, acc[K + j]);
+      }
+    }
+    if constexpr (TWO) {
+      int p = 0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+#pragma unroll
+        for (int j = i + 1; j < K; ++j, ++p) {
+          if (j >= kv || !cd[i].ok || !cd[j].ok || cd[i].g != cd[j].g) continue;
+          double* e = acc + 2 * K + 3 * p;
+          const bool plane = cd[i].ch == cd[j].ch;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            e[0] = fma((double)dI[i][k], (double)dI[j][k], e[0]);
+            if (plane) {
+              const float x = 2.0f * cd[i].delta * cd[j].delta * invp *
+                              fmaf(lh[i][2 * k], lh[j][2 * k], lh[i][2 * k + 1] * lh[j][2 * k + 1]);
+              e[1] = fma((double)x, (double)lt[j][k], e[1]);
+              const float s2 = 2.0f * (li[j][k] + dI[i][k] + dI[j][k]) + x;
+              e[2] = fma((double)s2, (double)x, e[2]);
+            }
+          }
+        }
+      }
+    }
+  }
+  HBX_TT(2);
+  block_sum_lds<NT>(acc, red_all, red_seg, tot);
+  HBX_TT(3);
+  // partials out as write-through stores (cache policy sc1), read back by the deciding
+  // block with sc1 loads (buffer ops: the loads of all partials are in flight together)
+  const __amdgpu_buffer_rsrc_t rp = wave_rsrc(a.partial, (unsigned)(gridDim.x * NT * sizeof(double)));
+#ifdef HBX_WALK_TIMING
+  if (threadIdx.x == 0) {   // per-block start and state-load latency (debug slots after the partials)
+    long long* dbg = reinterpret_cast<long long*>(a.partial + NT * gridDim.x);
+    __hip_atomic_store(dbg + 2 * blockIdx.x, (long long)tt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(dbg + 2 * blockIdx.x + 1, (long long)(tt[8] - tt[0]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
+  // term-major ([NT][blocks]): the deciding block's lanes then read consecutive words
+  if ((int)threadIdx.x < NT)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(walk_u32x2, tot[threadIdx.x]), rp,
+                                          (int)((threadIdx.x * gridDim.x + blockIdx.x) * sizeof(double)), 0, kSc1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // arrival in two levels, the counter sharded by blockIdx % 8 (the blocks that share
+    // an XCD under round-robin placement -- a speed hint only): the last arriver of each
+    // shard adds to counter[0], whose last arriver decides
+#ifndef HBX_WALK_TWO_LEVEL
+    s_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+#else
+    const int ng = (int)gridDim.x < 8 ? (int)gridDim.x : 8;
+    const int r = (int)blockIdx.x % 8;
+    const int gsz = ((int)gridDim.x - r + 7) / 8;
+    const int ticket = __hip_atomic_fetch_add(counter + 1 + r, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = 0;
+    if (ticket == gsz - 1)
+      last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    s_last = last;
+#endif
+  }
+  __syncthreads();
+  if (!s_last) return;
+  HBX_TT(4);
+
+  // ---- the last block: every partial (fixed order), the PSNRs, the decision ----
+  const int tid = threadIdx.x;
+  // issued together: the next actions' mask words, the base statistics, every partial
+  int nch = -1, npix = 0;
+  uint64_t nwd = 0;
+  if (tid < nn && nact >= 0 && nact < (int64_t)CH * (int64_t)hw) {
+    nch = (int)(nact / (int64_t)hw);
+    npix = (int)(nact % (int64_t)hw);
+    nwd = a.mask[((size_t)nch * N + npix / N) * (N / 64) + (npix % N) / 64];
+  }
+  double bs[3 * NG];
+#pragma unroll
+  for (int i = 0; i < 3 * NG; ++i) bs[i] = i < 3 * G ? a.base_stats[i] : 0.0;
+  double v[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) v[t] = 0.0;
+  for (int b = tid; b < (int)gridDim.x; b += kWalkNT) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      v[t] += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                             rp, (int)((t * gridDim.x + b) * sizeof(double)), 0, kSc1));
+  }
+  if (tid < nn) {
+    s_nch[tid] = nch;
+    s_npix[tid] = npix;
+    s_nwd[tid] = nwd;
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) s_cd[j] = cd[j];
+  }
+  HBX_TT(5);
+  block_sum_lds<NT>(v, red_all, red_seg, tot);
+  HBX_TT(6);
+  // the PSNRs: lane j < K = candidate j on the base, lane K + p = pair p = (i, j), i < j,
+  // both flips on the base (the state after accepting i, then j) -- the summation order
+  // of a serial pass, so the decision is the same
+  auto psnr_of = [&](const double (&st)[3 * NG]) {
+    double sxy = 0.0, sxx = 0.0, syy = 0.0;
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg) {
+      if (gg >= G) break;
+      sxy += st[3 * gg]; sxx += st[3 * gg + 1]; syy += st[3 * gg + 2];
+    }
+    return psnr_from(sxy, sxx, syy, a.count, a.rel, a.peak);
+  };
+  // adds candidate i's increments (and, for the second of a pair in the same group, the
+  // pair terms) to st in place
+  auto add_cand = [&](double (&st)[3 * NG], int i) {
+    const int g = s_cd[i].g;
+    const double dxy = tot[i], dxx = tot[K + i];
+#pragma unroll
+    for (int gg = 0; gg < NG; ++gg) {     // unconditional adds (+ 0 elsewhere): no indexed
+      st[3 * gg] += gg == g ? dxy : 0.0;   // access, which would put st in scratch
+      st[3 * gg + 1] += gg == g ? dxx : 0.0;
+    }
+  };
+  auto add_pair = [&](double (&st)[3 * NG], int i, int j) {
+    const int g = s_cd[j].g;
+    add_cand(st, j);
+    if (g == s_cd[i].g) {
+      const int p = i * (2 * K - i - 1) / 2 + (j - i - 1);   // index of (i < j), row-major
+      const double dxy = tot[2 * K + 3 * p + 1], dxx = 2.0 * tot[2 * K + 3 * p] + tot[2 * K + 3 * p + 2];
+#pragma unroll
+      for (int gg = 0; gg < NG; ++gg) {
+        st[3 * gg] += gg == g ? dxy : 0.0;
+        st[3 * gg + 1] += gg == g ? dxx : 0.0;
+      }
+    }
+  };
+  if (tid < K + NP) {
+    int i = tid, j = -1;
+    if (tid >= K) {                      // pair index -> (i, j)
+      int p = tid - K;
+      i = 0;
+      while (p >= K - 1 - i) { p -= K - 1 - i; ++i; }
+      j = i + 1 + p;
+    }
+    double ps = NAN;
+    if (i < kv && s_cd[i].ok && (j < 0 || (j < kv && s_cd[j].ok))) {
+      double st[3 * NG];
+#pragma unroll
+      for (int e = 0; e < 3 * NG; ++e) st[e] = bs[e];
+      add_cand(st, i);
+      if (j >= 0) add_pair(st, i, j);
+      ps = psnr_of(st);
+    }
+    s_ps[tid] = ps;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  HBX_TT(9);
+  HBX_TT(10);
+  for (int i = 0; i < kWalkTickets; ++i)
+    __hip_atomic_store(counter + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  hbx_dbs_walk_t nw = ws;
+  nw.commit_ch = -1;
+  nw.commit_pix = 0;
+  nw.commit2_ch1 = 0;
+  nw.commit_pix2 = 0;
+  int64_t new_pos = pos;
+  int acc_j[2] = {-1, -1};
+  if (kv > 0) {
+    nw.batches += 1;
+    double prev = ws.prev_psnr, last = NAN;
+    int64_t n_acc = ws.accepted;
+    new_pos = pos + kv;
+    bool stop = false;
+    double acc_ps[2] = {NAN, NAN};
+    int a0 = -1;
+    for (int j = 0; j < kv; ++j) {         // first accept against the base
+      last = s_ps[j];
+      if (last > prev) { a0 = j; break; }  // strict (DBS_1024_24.py:355); NaN never
+    }
+    if (a0 >= 0) {
+      double fin[3 * NG];
+#pragma unroll
+      for (int e = 0; e < 3 * NG; ++e) fin[e] = bs[e];
+      add_cand(fin, a0);
+      prev = last;
+      acc_j[0] = a0;
+      acc_ps[0] = last;
+      new_pos = pos + a0 + 1;
+      const bool halt0 = ws.refresh_every > 0 && (n_acc + 1) % ws.refresh_every == 0;
+      const bool stop0 = ws.stop_enabled && prev - ws.init_psnr >= ws.stop_diff;   // DBS_ratio_0.5.py:366-372
+      n_acc += 1;
+      stop = stop0;
+      if (halt0) nw.halt = 1;
+      if constexpr (TWO) {
+        if (!halt0 && !stop0) {            // second accept: candidates after a0 on the state with a0
+          const WalkCand c0 = s_cd[a0];
+          new_pos = pos + kv;
+          for (int j = a0 + 1; j < kv; ++j) {
+            const WalkCand cj = s_cd[j];
+            if (cj.ok && cj.ch == c0.ch && cj.pix == c0.pix) { new_pos = pos + j; break; }
+            last = s_ps[K + a0 * (2 * K - a0 - 1) / 2 + (j - a0 - 1)];
+            if (last > prev) {
+              acc_j[1] = j;
+              acc_ps[1] = last;
+              add_pair(fin, a0, j);
+              prev = last;
+              new_pos = pos + j + 1;
+              if (ws.refresh_every > 0 && (n_acc + 1) % ws.refresh_every == 0) nw.halt = 1;
+              if (ws.stop_enabled && prev - ws.init_psnr >= ws.stop_diff) stop = true;
+              n_acc += 1;
+              break;
+            }
+          }
+        }
+      }
+      HBX_TT(10);
+      // apply the accepts: mask bits, group sums, log, commits for the next launch
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int j = acc_j[s2];
+        if (j < 0) break;
+        const WalkCand cj = s_cd[j];
+        atomicXor(reinterpret_cast<unsigned long long*>(a.mask) + ((size_t)cj.ch * N + cj.r) * (N / 64) + cj.col / 64,
+                  1ull << (cj.col & 63));                                         // DBS_1024_24.py:320
+        const int64_t n = ws.accepted + s2;
+        if (n < a.log_cap) {
+          a.log_pos[n] = pos + j;
+          a.log_psnr[n] = acc_ps[s2];
+        }
+        if (s2 == 0) { nw.commit_ch = cj.ch; nw.commit_pix = cj.pix; }
+        else { nw.commit2_ch1 = cj.ch + 1; nw.commit_pix2 = cj.pix; }
+      }
+#pragma unroll
+      for (int i = 0; i < 3 * NG; ++i)
+        if (i < 3 * G) a.base_stats[i] = fin[i];                                   // :358-363
+    }
+    nw.accepted = n_acc;
+    nw.prev_psnr = prev;
+    if (!isnan(last)) nw.last_psnr = last;
+    nw.pos = new_pos;
+    if (stop) { nw.done = 1; nw.stopped_early = 1; }
+    if (nw.pos >= total) nw.done = 1;
+  }
+  HBX_TT(11);
+  // the next launch's actions and signs (the bits this batch flipped toggled)
+  WalkPre np;
+  np.pos = kv > 0 ? new_pos : -1;        // a commit-only launch decodes nothing
+  np.order = a.order;
+  np.n = 0;
+  np.pad = 0;
+  const int base = (int)(new_pos - pos - 1);
+#pragma unroll
+  for (int j = 0; j < kWalkPreMax; ++j) {
+    const int i = base + j;
+    const bool have = i >= 0 && i < nn;
+    const int ch = have ? s_nch[i] : -1, pix = have ? s_npix[i] : 0;
+    const uint64_t wd = have ? s_nwd[i] : 0;
+    np.ch[j] = ch;
+    np.pix[j] = pix;
+    if (have) np.n = j + 1;
+    const bool ok = ch >= 0;
+    int bit = (int)((wd >> ((pix % N) & 63)) & 1ull);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      if (acc_j[s2] >= 0) {
+        const WalkCand cj = s_cd[acc_j[s2]];
+        if (cj.ch == ch && cj.pix == pix) bit ^= 1;
+      }
+    np.delta[j] = ok ? a.vb * (float)(1 - 2 * bit) : 0.0f;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    np.cdelta[s2] = acc_j[s2] >= 0 ? s_cd[acc_j[s2]].delta : 0.0f;   // vb (2 bit' - 1) = vb (1 - 2 bit)
+  *prep = np;
+  *w = nw;
+#ifdef HBX_WALK_TIMING
+  HBX_TT(7);
+  if (nw.batches % 500 == 7) {
+    const unsigned long long t00 = tt[0];
+    printf("walk_step K %d batch %ld pre %d (10ns ticks from the deciding block's start): decider start %lld, state %lld, decode %lld, "
+           "pixels %lld, blocksum %lld, arrival %lld, gather %lld, sum2 %lld, psnr %lld, decided %lld, applied %lld, end %lld\n", K, (long)nw.batches,
+           (int)use_pre, (long long)(tt[0] - t00), (long long)(tt[8] - t00), (long long)(tt[1] - t00), (long long)(tt[2] - t00),
+           (long long)(tt[3] - t00), (long long)(tt[4] - t00), (long long)(tt[5] - t00), (long long)(tt[6] - t00),
+           (long long)(tt[9] - t00), (long long)(tt[10] - t00), (long long)(tt[11] - t00), (long long)(tt[7] - t00));
+    if (NT * gridDim.x + 2 * gridDim.x <= 6656) {
+      const long long* dbg = reinterpret_cast<const long long*>(a.partial + NT * gridDim.x);
+      long long s0 = 1ll << 62, s1 = -(1ll << 62), l0 = 1ll << 62, l1 = 0, lsum = 0;
+      int nslow = 0;
+      for (int b = 0; b < (int)gridDim.x; ++b) {
+        const long long st = __hip_atomic_load(dbg + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - (long long)t00;
+        const long long la = __hip_atomic_load(dbg + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s0 = st < s0 ? st : s0; s1 = st > s1 ? st : s1;
+        l0 = la < l0 ? la : l0; l1 = la > l1 ? la : l1; lsum += la;
+        nslow += la > 1000;
+      }
+      printf("   blocks: start [%lld, %lld], state latency min %lld max %lld mean %lld, >10us: %d\n", s0, s1, l0, l1,
+             lsum / (long long)gridDim.x, nslow);
+    }
+  }
+#endif
+}
+
 // blocks per candidate: enough blocks in flight to stream at full rate for
 // small K, never more than one quad per thread
 int walk_blocks_per_job(int N, int K) {
@@ -305,6 +885,17 @@ int walk_blocks_per_job(int N, int K) {
   int b = 1;
   while (b * K < 2048 && b < 1024) b *= 2;
   return b < max_b ? b : max_b;
+}
+
+// fused-step variants: K = 1 (single accept), 2..4 (two accepts resolved per batch);
+// other K run the split three-kernel batch (a fused step keeps every candidate's
+// loads of a quad in registers: beyond 4 candidates that spills)
+bool walk_fused_k(int K) { return K >= 1 && K <= 4; }
+
+int walk_step_blocks(int N) {
+  const int nq = N * N / 4;
+  const int b = (nq + kWalkNT - 1) / kWalkNT;          // one quad per thread at most
+  return b < kWalkStepBlocksMax ? b : kWalkStepBlocksMax;
 }
 
 hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
@@ -331,8 +922,28 @@ hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
   a.count = l.count;
   a.peak = l.peak;
   a.rel = l.rel;
+  a.commit_only = 0;
   const int nq = pd.N * pd.N / 4;
+  const dim3 grid((unsigned)walk_step_blocks(pd.N));
+  if (l.fused && walk_fused_k(l.K)) {
+    for (int b = 0; b < l.batches; ++b) {
+      switch (l.K) {
+        case 1: hipLaunchKernelGGL((k_walk_step<1, false>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
+        case 2: hipLaunchKernelGGL((k_walk_step<2, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
+        case 3: hipLaunchKernelGGL((k_walk_step<3, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
+        default: hipLaunchKernelGGL((k_walk_step<4, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
+      }
+    }
+    return hipGetLastError();
+  }
   const unsigned bpc = (unsigned)std::min(512, (nq + kWalkNT - 1) / kWalkNT);
+  if (l.fused && l.batches > 0) {
+    // commits a fused step left pending (the split eval reads field / intensity as they
+    // are): one commit-only step, which returns at once when there are none
+    WalkArgs c = a;
+    c.commit_only = 1;
+    hipLaunchKernelGGL((k_walk_step<1, false>), grid, dim3(kWalkNT), 0, st, c, l.counter);
+  }
   for (int b = 0; b < l.batches; ++b) {
     hipLaunchKernelGGL(k_walk_eval, dim3((unsigned)a.bpj, (unsigned)l.K), dim3(kWalkNT), 0, st, a);
     hipLaunchKernelGGL(k_walk_decide, dim3(1), dim3(kWalkNT), 0, st, a);

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 6
+ABI_VERSION = 7
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -23,6 +23,7 @@ ACCEPT_ENV, ACCEPT_DBS = 0, 1
 REWARD_PSNR, REWARD_IMPORTANCE = 0, 1
 MAX_GROUPS = 4
 WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
+WALK_FUSED_K = (1, 2, 3, 4)   # one launch per batch (two accepts resolved for K = 2..4)
 PRECISION_F32, PRECISION_BF16_STORE, PRECISION_F16_STORE = 0, 1, 2   # hbx_plan_set_precision
 
 EXPORTED_SYMBOLS = (
@@ -66,7 +67,8 @@ class DbsWalk(C.Structure):
         ("stop_diff", C.c_double),
         ("stop_enabled", C.c_int32), ("refresh_every", C.c_int32), ("done", C.c_int32), ("halt", C.c_int32),
         ("stopped_early", C.c_int32), ("commit_ch", C.c_int32), ("commit_pix", C.c_int32),
-        ("reserved", C.c_int32 * 3),
+        ("commit2_ch1", C.c_int32), ("commit_pix2", C.c_int32), ("split_ch1", C.c_int32),
+        ("split_pix", C.c_int32), ("reserved", C.c_int32),
     ]
 
 

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import io
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -68,17 +69,33 @@ def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
     return int(idx[0]) if idx.size else None
 
 
-def walk_k(q: float, n: int, k_min: int = 1, k_max: int = 256) -> int:
-    """Speculation depth of the device walk for acceptance rate q at side n:
-    the K minimising (per-batch overhead + K * per-candidate stream time) /
-    expected candidates consumed per batch, (1 - (1 - q)^K) / q."""
-    o = 12.0                          # us: two launches + the last block's decision
-    c = 16.0 * n * n / 5.0e6          # us: one candidate's 16 B/px at ~5 TB/s
+def walk_k(q: float, n: int, k_min: int = 1, k_max: int = 256, fused: bool = True) -> int:
+    """Speculation depth of the device walk for acceptance rate q at side n: the K
+    minimising (per-batch overhead + K * per-candidate stream time + accepts *
+    commit time) / expected candidates visited per batch.
+
+    fused (ABI v7): K in _lib.WALK_FUSED_K is one launch per batch, and for K = 2..4 the
+    batch runs to the SECOND accept (visited = sum_{k<=K} P(fewer than 2 accepts in
+    the first k-1)), otherwise to the first (sum_{k<=K} (1-q)^(k-1)).  Split (v5):
+    three launches, first accept only."""
+    c = 16.0 * n * n / 3.7e6          # us: one candidate's 16 B/px (~3.7 TB/s effective, measured)
+    cm = 24.0 * n * n / 5.5e6         # us: committing an accepted flip (24 B/px)
     q = min(max(q, 1e-6), 1.0)
+    p = 1.0 - q
     best, bk = math.inf, k_min
     for k in range(max(1, k_min), max(k_min, k_max) + 1):
-        vis = (1.0 - (1.0 - q) ** k) / q
-        cost = (o + k * c) / vis
+        one_launch = fused and k in _lib.WALK_FUSED_K      # larger K: the split three-launch batch
+        two = one_launch and k >= 2
+        if two:
+            vis = sum(p ** (i - 1) + (i - 1) * q * p ** max(i - 2, 0) for i in range(1, k + 1))
+            acc = (1.0 - p ** k) + (1.0 - p ** k - k * q * p ** (k - 1))     # min(2, accepts)
+        else:
+            vis = (1.0 - p ** k) / q
+            acc = 1.0 - p ** k
+        # us per batch besides the streaming: launch boundary + arrival + decision tail (one
+        # launch, measured 8.5 at 1024 x 24, DESIGN 4c) / three launches
+        o = 8.5 if one_launch else 14.0
+        cost = (o + k * c + acc * cm) / vis
         if cost < best:
             best, bk = cost, k
     return bk
@@ -121,6 +138,7 @@ class _Walk:
         w.stop_diff = float(stop_diff) if stop_diff is not None else 0.0
         w.refresh_every = int(refresh_every or 0)
         w.commit_ch = -1
+        w.commit2_ch1 = 0
         self.st = w
         nbytes = C.sizeof(_lib.DbsWalk)
         self.wbuf = torch.frombuffer(bytearray(bytes(w)), dtype=torch.uint8).to(dev)
@@ -131,7 +149,8 @@ class _Walk:
         self.events = [torch.cuda.Event(), torch.cuda.Event()]
         self.k_lo, self.k_hi = max(1, k_min), min(k_max, _lib.WALK_MAX_K)
         self.q, self.pos_prev, self.acc_prev = 0.5, 0, 0
-        self.k = walk_k(self.q, plan.cfg.height, self.k_lo, self.k_hi)
+        self.fused = os.environ.get("HBX_WALK_SPLIT", "0") in ("", "0")
+        self.k = walk_k(self.q, plan.cfg.height, self.k_lo, self.k_hi, self.fused)
         self.marks = []               # (accepts so far, seconds) per processed chunk
         self.exact = {}               # accept index -> exact PSNR after a refresh
         self.issued = self.done_n = 0
@@ -139,8 +158,11 @@ class _Walk:
         self.t0 = time.perf_counter()
 
     def _chunk(self, stream):
+        self._chunk_n(stream, self.chunk)
+
+    def _chunk_n(self, stream, batches):
         self.plan.dbs_walk_psf(self.mask, self.target, self.base_stats, self.field, self.inten, self.order_t,
-                               self.wbuf, self.log_pos, self.log_psnr, self.k, self.chunk, stream=stream)
+                               self.wbuf, self.log_pos, self.log_psnr, self.k, batches, stream=stream)
 
     def issue(self):
         slot = self.issued % 2
@@ -182,7 +204,7 @@ class _Walk:
         dpos, dacc = st.pos - self.pos_prev, st.accepted - self.acc_prev
         if dpos > 0:
             self.q = 0.5 * self.q + 0.5 * (dacc / dpos)
-            self.k = walk_k(self.q, self.plan.cfg.height, self.k_lo, self.k_hi)
+            self.k = walk_k(self.q, self.plan.cfg.height, self.k_lo, self.k_hi, self.fused)
         self.pos_prev, self.acc_prev = st.pos, st.accepted
         if st.halt:
             while self.done_n < self.issued:   # the chunk behind it saw halt: no-ops
@@ -198,6 +220,7 @@ class _Walk:
                 self.inten.copy_(it[0])
                 st.prev_psnr = float(ps_exact.item())
                 st.halt = 0
+                st.commit_ch, st.commit2_ch1 = -1, 0     # the mask holds them: the refresh applied them
                 self.exact[int(st.accepted) - 1] = st.prev_psnr
                 self.wbuf.copy_(torch.frombuffer(bytearray(bytes(st)), dtype=torch.uint8))
             if st.done:
@@ -214,6 +237,11 @@ class _Walk:
         self.issue()
 
     def _finish(self):
+        # the fused walk step applies a batch's accepted flips in the NEXT launch: one more
+        # (commit-only) launch brings field / intensity up to the final mask
+        self.k = 1
+        self._chunk_n(self.s, 1)
+        self.s.synchronize()
         self.finished = True
         self.seconds = time.perf_counter() - self.t0
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 6
+#define HBX_ABI_VERSION 7
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -246,10 +246,23 @@ int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_
  * serial loop's: every candidate before an accepted one was evaluated against
  * exactly the state the serial loop would have had.
  *
- * The walk state lives in DEVICE memory (caller-owned; commit_ch = -1 and the
- * counters zero at the start); the caller reads it back between calls.  When halt == 1
- * (after every refresh_every-th accept) the caller re-propagates field,
- * intensity and base_chan_stats exactly (hbx_simulate / hbx_propagate), sets
+ * ABI v7: for K in {1, 2, 3, 4, 6, 8, 12, 16} a batch is ONE launch (k_walk_step):
+ * it first applies the previous batch's accepted flip(s) to field / intensity,
+ * evaluates the K candidates on the updated state, and its last-arriving
+ * workgroup decides; for K = 2..4 it also resolves the first candidate after
+ * the first accept against the state WITH that accept (exact pairwise terms),
+ * so a batch takes up to two accepts of the serial loop.  The accepted flips of
+ * a batch therefore reach field / intensity in the NEXT launch: after the walk
+ * is done make one more call (batches >= 1; it only commits).  Other K run the
+ * three-launch batch of ABI v5 (eval / decide / commit; also selected for every
+ * K by HBX_WALK_SPLIT=1 in the environment at plan creation).
+ *
+ * The walk state lives in DEVICE memory (caller-owned; commit_ch = -1,
+ * commit2_ch1 = 0, split_ch1 = 0 and the counters zero at the start); the caller reads it back
+ * between calls.  When halt == 1 (after every refresh_every-th accept) the
+ * caller re-propagates field, intensity and base_chan_stats exactly
+ * (hbx_simulate / hbx_propagate) -- the mask already holds every accepted flip,
+ * so it also drops pending commits (commit_ch = -1, commit2_ch1 = 0) -- sets
  * prev_psnr to the exact PSNR and clears halt.
  * n_order (ABI v6) is the length of `order`: the walk never visits past
  * min(walk->total, n_order).
@@ -275,7 +288,13 @@ typedef struct hbx_dbs_walk {
   int32_t stopped_early;
   int32_t commit_ch;       /* internal: pending commit channel, -1 = none        */
   int32_t commit_pix;      /* internal                                           */
-  int32_t reserved[3];     /* zero                                               */
+  int32_t commit2_ch1;     /* internal (ABI v7): channel + 1 of a second pending
+                              commit, 0 = none                                   */
+  int32_t commit_pix2;     /* internal                                           */
+  int32_t split_ch1;       /* internal (ABI v7): channel + 1 of the split batch's
+                              accept, applied within the batch, 0 = none          */
+  int32_t split_pix;       /* internal                                           */
+  int32_t reserved;        /* zero                                               */
 } hbx_dbs_walk_t;
 int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
                      double* base_chan_stats, float* field, float* intensity, const int64_t* order,

@@ -218,3 +218,43 @@ def test_bf16_intermediates_deviation_256(golden_dir):
     print(f"bf16 run: {res.steps} candidates to +0.5 dB (oracle {int(d['n'])}), final PSNR error {dev_final:.2e} dB")
     assert dev_final <= 5e-2
     plan.close()
+
+
+def test_split_walk_batches_equal_oracle(golden_dir, monkeypatch):
+    """The ABI v5 three-launch batches (HBX_WALK_SPLIT=1 at plan creation) still give the
+    oracle's accept sequence -- the fused one-launch step is the default."""
+    from hbx import dbs
+    monkeypatch.setenv("HBX_WALK_SPLIT", "1")
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24.npz")
+    n = 2048
+    plan, mask, target = _dev(ocfg, pre, tgt)
+    res = dbs.greedy(plan, mask, target, order[:n], mode="psf")
+    assert _first_difference(res.accepted_positions, d["accepted"][:n]) is None
+    assert _gain_error(res, d, n) <= GAIN_TOL_DB
+    plan.close()
+
+
+@pytest.mark.parametrize("refresh", [4096, 256])
+def test_walk_mixed_k_fused_and_split_equal_oracle(golden_dir, monkeypatch, refresh):
+    """The speculation depth changes between chunks (walk_k follows the acceptance
+    rate): fused one-launch steps (K <= 4, commits applied by the NEXT launch) and
+    split three-launch batches (K > 4, commit inside the batch) interleave in one walk.
+    Cycling K through both kinds every chunk still gives the oracle's accept
+    sequence and mask -- no pending commit lost or applied twice at a switch."""
+    from hbx import dbs
+    ks = [3, 8, 1, 32, 2, 4, 5, 2]
+    it = iter(range(10 ** 6))
+    monkeypatch.setattr(dbs, "walk_k", lambda *a, **k: ks[next(it) % len(ks)])
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24.npz")
+    n = 4096
+    plan, mask, target = _dev(ocfg, pre, tgt)
+    res = dbs.greedy(plan, mask, target, order[:n], mode="psf", refresh_every=refresh)
+    first = _first_difference(res.accepted_positions, d["accepted"][:n])
+    assert first is None, (first, float(d["delta"][first]))
+    assert res.steps == n
+    assert _gain_error(res, d, n) <= GAIN_TOL_DB
+    want = (pre >= 0.5).astype(np.uint8)
+    c, r, col = O.decode_action(order[:n][d["accepted"][:n]], ocfg.height, ocfg.width)
+    np.bitwise_xor.at(want, (c, r, col), 1)
+    assert np.array_equal(mask.cpu().numpy().view("<u8"), O.pack_mask(want))
+    plan.close()

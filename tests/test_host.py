@@ -209,5 +209,9 @@ def test_walk_k_choice():
     assert walk_k(0.5, 1024) <= 4
     assert walk_k(0.01, 1024) > walk_k(0.5, 1024)
     assert walk_k(0.5, 64) > walk_k(0.5, 1024)
-    assert walk_k(1e-9, 1024, 1, 256) == 256
+    assert walk_k(1e-9, 1024, 1, 256, fused=False) == 256
+    assert walk_k(1e-9, 1024, 1, 256) == 256           # rare accepts: long split batches
     assert 1 <= walk_k(1.0, 1024) <= 2
+    from hbx import _lib
+    for q in (0.9, 0.5, 0.3):                          # frequent accepts: one-launch two-accept steps
+        assert walk_k(q, 1024) in _lib.WALK_FUSED_K

@@ -13,6 +13,10 @@ import torch  # noqa: E402
 import hbx  # noqa: E402
 from hbx import dbs  # noqa: E402
 
+if os.environ.get("WALK_PROF_K"):              # fixed speculation depth (timing experiments)
+    _fixed_k = int(os.environ["WALK_PROF_K"])
+    dbs.walk_k = lambda *a, **k: _fixed_k
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 mode = sys.argv[2] if len(sys.argv) > 2 else "psf"
 many = int(sys.argv[3]) if len(sys.argv) > 3 else 0     # > 0: that many images via dbs.greedy_many
