@@ -69,6 +69,30 @@ def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
     return int(idx[0]) if idx.size else None
 
 
+def rgb_artifact_paths(file_name: str, dbs_folder: str = "DBS"):
+    """The reconstructed-RGB files DBS_1024_24.py writes per image, names verbatim
+    (`:283` has 'png' before '_rgb_before', `:447` does not): (before, after)."""
+    return (os.path.join(dbs_folder, f"episode_{file_name}png_rgb_before.npy"),
+            os.path.join(dbs_folder, f"episode_{file_name}_rgb_after.npy"))
+
+
+def save_rgb(plan: Plan, mask: torch.Tensor, target: torch.Tensor, path: str, stream=None) -> np.ndarray:
+    """np.save of the reconstructed RGB the reference saves before and after its greedy loop
+    (DBS_1024_24.py:252-257 + :280-286 / :444-451): per colour group the plane mean of
+    |tt.simulate|^2, float32 [1, G, H, W], from one exact propagation of ``mask``.  Prints the
+    reference's 'RGB data saved to ...' line; returns the array."""
+    inten, _, _ = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=True, stream=stream)
+    if stream is not None:
+        stream.synchronize()
+    rgb = inten.float().cpu().numpy()                      # [1, G, H, W]
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    np.save(path, rgb)
+    print(f"RGB data saved to {path}")
+    return rgb
+
+
 def walk_k(q: float, n: int, k_min: int = 1, k_max: int = 256, fused: bool = True) -> int:
     """Speculation depth of the device walk for acceptance rate q at side n: the K
     minimising (per-batch overhead + K * per-candidate stream time + accepts *

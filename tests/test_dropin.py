@@ -254,3 +254,34 @@ def test_dbs_1024_24_driver_statements_unchanged():
         assert np.array_equal(current_state[0], lg.state)
         assert previous_psnr == pytest.approx(lg.previous_psnr, abs=1e-5)
     env.close()
+
+
+def test_dbs_rgb_artifacts(tmp_path, capsys):
+    """DBS_1024_24.py:280-286 / :444-451: the reconstructed RGB saved before and after the
+    greedy loop, under the reference's file names, equal to the oracle's group means."""
+    import hbx
+    from hbx import dbs
+    ocfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    pre, tgt = O.synthetic_inputs(ocfg, 11)
+    cfg = hbx.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    plan = hbx.Plan(cfg, max_jobs=16)
+    mask = hbx.pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+    target = torch.from_numpy(tgt).cuda()
+    before, after = dbs.rgb_artifact_paths("0801", str(tmp_path / "DBS"))
+    assert before.endswith("DBS/episode_0801png_rgb_before.npy") and after.endswith("DBS/episode_0801_rgb_after.npy")
+    m0 = (pre >= 0.5).astype(np.float32)
+    dbs.save_rgb(plan, mask, target, before)
+    order = np.random.default_rng(5).permutation(ocfg.channels * 64 * 64)[:300]
+    res = dbs.greedy(plan, mask, target, order, mode="psf")
+    dbs.save_rgb(plan, mask, target, after)
+    out = capsys.readouterr().out
+    assert f"RGB data saved to {before}" in out and f"RGB data saved to {after}" in out
+    prop = O.Propagator(ocfg)
+    m1 = O.unpack_mask(mask.cpu().numpy().view("<u8"), 64).astype(np.float32)
+    assert int(np.sum(m1 != m0)) == len(res.accepted_positions)
+    for path, m in ((before, m0), (after, m1)):
+        got = np.load(path)
+        want = prop.all_intensity(m)[None]
+        assert got.shape == (1, 3, 64, 64) and got.dtype == np.float32
+        assert np.max(np.abs(got - want)) <= 2e-5 * np.max(want)
+    plan.close()
