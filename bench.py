@@ -190,8 +190,9 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                                "psnr_gain_db": round(r2.final_psnr - r2.initial_psnr, 6),
                                "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1),
                                "batches": r2.launches,
-                               "walk": "device-resident (hbx_dbs_walk_psf): eval, one-block decide and commit launches per batch, "
-                                       "one host sync per 64 batches",
+                               "walk": "device-resident (hbx_dbs_walk_psf): one launch per batch for K <= 4 (the previous "
+                                       "batch's commits, K candidates with pair terms, last-arriving block decides up to two "
+                                       "accepts), three launches for larger K; one host sync per 64 batches",
                                "host_decided_batches": {
                                    "flips_per_s": round(r3.steps / dt3, 1), "seconds": round(dt3, 3),
                                    "batches": r3.launches,
