@@ -127,6 +127,7 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     import torch
     from hbx import dbs
     from hbx.plan import Plan
+    from hbx.plan import pack_bits as hbx_pack
     CH, N = cfg.channels, cfg.height
     order = np.random.default_rng(3).permutation(CH * N * N)[:n_flips]
     plan = Plan(cfg, max_jobs=256)
@@ -181,6 +182,27 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                                      it4[0].contiguous(), cand)
         first_change = float((ps4 - p4).item())
     plan.close()
+    # several images side by side (DBS_1024_24.py loops over a folder, :208-211): one walk per
+    # image, each with its own plan and stream (hbx.dbs.greedy_many)
+    n_img = 4
+    plans = [Plan(cfg, max_jobs=cfg.groups) for _ in range(n_img)]
+    gens = [torch.Generator(device=mask.device).manual_seed(100 + i) for i in range(n_img)]
+    masks = [hbx_pack(torch.rand((CH, N, N), generator=gg, device=mask.device) >= 0.5) for gg in gens]
+    tgts = [torch.rand((cfg.groups, N, N), generator=gg, device=mask.device) for gg in gens]
+    orders = [np.random.default_rng(3 + i).permutation(CH * N * N)[:n_flips] for i in range(n_img)]
+    dbs.greedy_many(plans, [m.clone() for m in masks], tgts, [o[:256] for o in orders])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rm = dbs.greedy_many(plans, masks, tgts, orders)
+    torch.cuda.synchronize()
+    dtm = time.perf_counter() - t0
+    for pl in plans:
+        pl.close()
+    many = {"images": n_img, "flips": sum(r.steps for r in rm), "seconds": round(dtm, 3),
+            "flips_per_s_aggregate": round(sum(r.steps for r in rm) / dtm, 1),
+            "accepted": sum(len(r.accepted_positions) for r in rm),
+            "note": "hbx.dbs.greedy_many: one device walk per image (own plan and HIP stream), same prefix "
+                    "length per image, synthetic seeded images"}
     out["incremental_mode"] = {"flips": r2.steps, "seconds": round(dt2, 3),
                                "flips_per_s": round(r2.steps / dt2, 1), "accepted": len(r2.accepted_positions),
                                "same_accepts_as_fft_mode": bool(len(diff) == 0),
@@ -190,6 +212,7 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                                "psnr_gain_db": round(r2.final_psnr - r2.initial_psnr, 6),
                                "full_sweep_extrapolated_s": round(CH * N * N / (r2.steps / dt2), 1),
                                "batches": r2.launches,
+                               "several_images": many,
                                "walk": "device-resident (hbx_dbs_walk_psf): one launch per batch for K <= 4 (the previous "
                                        "batch's commits, K candidates with pair terms, last-arriving block decides up to two "
                                        "accepts), three launches for larger K; one host sync per 64 batches",
