@@ -266,6 +266,11 @@ int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_
  * prev_psnr to the exact PSNR and clears halt.
  * n_order (ABI v6) is the length of `order`: the walk never visits past
  * min(walk->total, n_order).
+ * The walk's partial sums, arrival counters and decoded next actions live in
+ * plan-owned scratch: at most one walk per plan may be in flight at a time
+ * (walks of several images side by side need one plan each, as
+ * hbx.dbs.greedy_many enforces); each call re-derives the decoded actions
+ * from `order` once, so a new walk on the same plan needs no reset.
  *
  * Candidate evaluation is in increment form: each candidate's f64 partials
  * are sum dI T and sum (2 I + dI) dI with dI = delta (2 Re(U conj h) +
