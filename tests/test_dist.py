@@ -121,3 +121,58 @@ def test_gloo_world2_sharded_probe_sweep():
         assert np.allclose(r[4], want.delta_bins, rtol=1e-12, atol=1e-15)
         assert r[5] == int(np.count_nonzero(want.improved))
     assert np.allclose(res[0][6] + res[1][6], want.psnr, rtol=0, atol=1e-12)
+
+
+def _dbs_worker(rank, world, port, out, tmp):
+    """hbx.dbs.greedy_dataset over 2 gloo ranks with the per-image walk replaced by a
+    deterministic stand-in (the walk itself is GPU-tested): image i runs on rank i % 2,
+    rank 0 receives every image's summary in image order."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "binary-hologram-reinforcement-learning_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from hbx import dist as hd
+    from hbx import dbs
+    hd.init(backend="gloo")
+    seen = []
+
+    def fake_many(plans, masks, targets, orders, **kw):
+        seen.append([int(m) for m in masks])
+        return [dbs.GreedyResult(initial_psnr=10.0 + m, final_psnr=11.0 + m, steps=len(o),
+                                 accepted_positions=list(range(m % 3)), accepted_psnr=[0.5] * (m % 3),
+                                 launches=1, stopped_early=(m == 4), seconds=0.25 * m)
+                for m, o in zip(masks, orders)]
+
+    dbs.greedy_many = fake_many
+    res = dbs.greedy_dataset(5, lambda i: (i, None), lambda i: list(range(100 + i)), lambda: object(),
+                             per_gpu=2, save_dir=os.path.join(tmp, f"r{rank}"))
+    hd.barrier()
+    out.put((rank, seen, res))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_dbs_dataset_sharding(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dbs_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (s, res)) for r, s, res in (q.get(timeout=100) for _ in procs))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert got[0][0] == [[0, 2], [4]] and got[1][0] == [[1, 3]]       # per_gpu = 2 side by side
+    assert got[1][1] is None
+    rows = got[0][1]
+    assert [d["image"] for d in rows] == [0, 1, 2, 3, 4]
+    assert [d["rank"] for d in rows] == [0, 1, 0, 1, 0]
+    assert [d["candidates"] for d in rows] == [100, 101, 102, 103, 104]
+    assert [d["accepted"] for d in rows] == [0, 1, 2, 0, 1]
+    assert [d["final_psnr"] for d in rows] == [11.0, 12.0, 13.0, 14.0, 15.0]
+    assert [d["stopped_early"] for d in rows] == [False, False, False, False, True]
+    import numpy as np
+    z = np.load(tmp_path / "r1" / "dbs_image3_accepted.npz")
+    assert z["positions"].tolist() == [] and (tmp_path / "r0" / "dbs_image4_accepted.npz").exists()

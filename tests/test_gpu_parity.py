@@ -757,6 +757,34 @@ def test_dbs_greedy_many_equals_single_walks():
         p.close()
 
 
+def test_dbs_dataset_single_rank_equals_single_walks(tmp_path):
+    """dbs.greedy_dataset (the per-folder loop, images sharded over ranks; world 1 here)
+    gives each image exactly its greedy(mode="psf") result, two images side by side."""
+    import hbx
+    from hbx import dbs
+    ocfg = small_rgb()
+    cfg = dev_cfg(ocfg)
+    n = ocfg.channels * 64 * 64
+    ins = [O.synthetic_inputs(ocfg, 80 + i) for i in range(3)]
+    orders = [np.random.default_rng(90 + i).permutation(n)[:2000] for i in range(3)]
+
+    def load(i):
+        return hbx.pack_bits(torch.from_numpy(ins[i][0]).cuda() >= 0.5), torch.from_numpy(ins[i][1]).cuda()
+
+    rows = dbs.greedy_dataset(3, load, lambda i: orders[i], lambda: hbx.Plan(cfg, max_jobs=cfg.groups),
+                              per_gpu=2, save_dir=str(tmp_path))
+    assert [r["image"] for r in rows] == [0, 1, 2] and all(r["rank"] == 0 for r in rows)
+    for i, r in enumerate(rows):
+        plan = hbx.Plan(cfg, max_jobs=cfg.groups)
+        m, t = load(i)
+        w = dbs.greedy(plan, m, t, orders[i], mode="psf")
+        plan.close()
+        assert r["accepted"] == len(w.accepted_positions) and r["final_psnr"] == w.final_psnr
+        assert r["candidates"] == w.steps == 2000
+        z = np.load(tmp_path / f"dbs_image{i}_accepted.npz")
+        assert z["positions"].tolist() == w.accepted_positions
+
+
 @pytest.mark.parametrize("field_kind", [0, 1])
 def test_dbs_walk_matches_host_batches_1024(field_kind):
     """1024 x 24 RGB: the device-resident walk and the host-decided psf batches
