@@ -117,6 +117,29 @@ def test_incremental_greedy_1024x24_equals_oracle(golden_dir, name, mode, refres
     plan.close()
 
 
+@pytest.mark.parametrize("refresh", [4096, 256])
+def test_incremental_greedy_1024x24_16k_equals_oracle(golden_dir, refresh):
+    """The device walk over a 16,384-candidate prefix of the 1024x24 sweep (the float64
+    oracle's run, dbs_prefix_1024x24_16k.npz): every decision the oracle's, with and
+    without exact refreshes."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
+    n = int(d["n"])
+    plan, mask, target = _dev(ocfg, pre, tgt)
+    res = dbs.greedy(plan, mask, target, order[:n], mode="psf", refresh_every=refresh)
+    first = _first_difference(res.accepted_positions, d["accepted"])
+    assert first is None, (first, float(d["delta"][first]))
+    assert res.steps == n
+    gerr = _gain_error(res, d, n)
+    print(f"16k prefix refresh={refresh}: {len(res.accepted_positions)} accepts, gain error {gerr:.2e} dB")
+    assert gerr <= GAIN_TOL_DB
+    want = (pre >= 0.5).astype(np.uint8)
+    c, r, col = O.decode_action(order[:n][d["accepted"]], ocfg.height, ocfg.width)
+    np.bitwise_xor.at(want, (c, r, col), 1)
+    assert np.array_equal(mask.cpu().numpy().view("<u8"), O.pack_mask(want))
+    plan.close()
+
+
 def test_fft_greedy_1024x24_vs_oracle(golden_dir):
     """FFT mode (every candidate a full f32 re-propagation of its group): the
     oracle's accept sequence up to the first candidate whose change lies within

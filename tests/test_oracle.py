@@ -281,3 +281,19 @@ def test_large_dbs_fixtures_reproduce(golden_dir, name, n_check):
     acc, ps, delta = lg.run(order)
     assert np.array_equal(acc, d["accepted"][:n_check])
     assert np.allclose(delta, d["delta"][:n_check], rtol=0, atol=1e-12)
+
+
+def test_long_dbs_prefix_extends_the_4096_fixture(golden_dir):
+    """dbs_prefix_1024x24_16k.npz (16,384 candidates) and dbs_prefix_1024x24.npz (4,096)
+    come from the same seeded image and order: the long run's first 4,096 decisions,
+    PSNRs and changes are the short one's."""
+    import os
+    a = np.load(os.path.join(golden_dir, "dbs_prefix_1024x24.npz"), allow_pickle=False)
+    b = np.load(os.path.join(golden_dir, "dbs_prefix_1024x24_16k.npz"), allow_pickle=False)
+    n = int(a["n"])
+    assert int(b["n"]) == 16384 and n == 4096
+    for k in ("seed", "order_seed", "size", "groups", "planes", "field_kind"):
+        assert int(a[k]) == int(b[k])
+    assert np.array_equal(a["accepted"], b["accepted"][:n])
+    assert np.array_equal(a["psnr"], b["psnr"][:n]) and np.array_equal(a["delta"], b["delta"][:n])
+    assert float(a["initial_psnr"]) == float(b["initial_psnr"])
