@@ -140,12 +140,13 @@ def test_incremental_greedy_1024x24_16k_equals_oracle(golden_dir, refresh):
     plan.close()
 
 
-def test_fft_greedy_1024x24_vs_oracle(golden_dir):
+@pytest.mark.parametrize("name", ["dbs_prefix_1024x24.npz", "dbs_prefix_1024x24_16k.npz"])
+def test_fft_greedy_1024x24_vs_oracle(golden_dir, name):
     """FFT mode (every candidate a full f32 re-propagation of its group): the
     oracle's accept sequence up to the first candidate whose change lies within
-    the f32 FFT resolution FFT_TOL_DB (none in this prefix on MI355X so far)."""
+    the f32 FFT resolution FFT_TOL_DB."""
     from hbx import dbs
-    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24.npz")
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, name)
     n = int(d["n"])
     plan, mask, target = _dev(ocfg, pre, tgt)
     res = dbs.greedy(plan, mask, target, order[:n], mode="fft")
