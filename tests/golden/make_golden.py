@@ -160,12 +160,12 @@ def dbs_prefix_large(cfg, n, seed=0, order_seed=3, stop_diff=None, n_probe=0):
 
 def build_large(only=()):
     """The headline-size fixtures (minutes of CPU; not rebuilt by the CPU tests):
-    DBS_1024_24.py greedy prefixes (amplitude 4096 and 16384 candidates, phase 1024) and the
+    DBS_1024_24.py greedy prefixes (amplitude 4096 and 16384 candidates, phase 4096) and the
     literal DBS_ratio_0.5.py run (256x256x8 mono until +0.5 dB, :366-372)."""
     specs = {
         "dbs_prefix_1024x24.npz": lambda: dbs_prefix_large(O.rgb_config(1024), 4096, n_probe=512),
         "dbs_prefix_1024x24_phase.npz":
-            lambda: dbs_prefix_large(O.rgb_config(1024, field_kind=O.FIELD_PHASE), 1024),
+            lambda: dbs_prefix_large(O.rgb_config(1024, field_kind=O.FIELD_PHASE), 4096),
         "dbs_ratio05_256.npz": lambda: dbs_prefix_large(O.mono_config(256), None, stop_diff=0.5),
         # the same amplitude prefix four times longer (~15 min of CPU): its first 4096
         # candidates are dbs_prefix_1024x24.npz's

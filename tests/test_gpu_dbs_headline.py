@@ -11,7 +11,7 @@ re-propagating oracle in tests/test_oracle.py) over
   dbs_prefix_1024x24.npz        the first 4096 candidates of rng(3).permutation(24 * 1024^2)
                                 on the seed-0 synthetic image (amplitude field), plus the
                                 change of the first 512 candidates against the initial state
-  dbs_prefix_1024x24_phase.npz  1024 candidates, binary-phase field
+  dbs_prefix_1024x24_phase.npz  4096 candidates, binary-phase field
   dbs_ratio05_256.npz           DBS_ratio_0.5.py's literal run (BASELINE configs[4]):
                                 256x256x8 mono until the PSNR has risen 0.5 dB (:366-372)
 
