@@ -167,6 +167,8 @@ def build_large(only=()):
         "dbs_prefix_1024x24_phase.npz":
             lambda: dbs_prefix_large(O.rgb_config(1024, field_kind=O.FIELD_PHASE), 4096),
         "dbs_ratio05_256.npz": lambda: dbs_prefix_large(O.mono_config(256), None, stop_diff=0.5),
+        # the 896 x 896 x 24 crop size (env_1024_24_128.py / DBS_1024_24-128.py), 2,048 candidates
+        "dbs_prefix_896x24.npz": lambda: dbs_prefix_large(O.rgb_config(896), 2048, seed=7),
         # the same amplitude prefix four times longer (~15 min of CPU): its first 4096
         # candidates are dbs_prefix_1024x24.npz's
         "dbs_prefix_1024x24_16k.npz": lambda: dbs_prefix_large(O.rgb_config(1024), 16384),

@@ -12,6 +12,7 @@ re-propagating oracle in tests/test_oracle.py) over
                                 on the seed-0 synthetic image (amplitude field), plus the
                                 change of the first 512 candidates against the initial state
   dbs_prefix_1024x24_phase.npz  4096 candidates, binary-phase field
+  dbs_prefix_896x24.npz         2048 candidates at the 896 x 896 x 24 crop size (seed 7)
   dbs_ratio05_256.npz           DBS_ratio_0.5.py's literal run (BASELINE configs[4]):
                                 256x256x8 mono until the PSNR has risen 0.5 dB (:366-372)
 
@@ -92,7 +93,7 @@ def _gain_error(res, d, upto):
     return float(np.max(np.abs(got - want)))
 
 
-@pytest.mark.parametrize("name", ["dbs_prefix_1024x24.npz", "dbs_prefix_1024x24_phase.npz"])
+@pytest.mark.parametrize("name", ["dbs_prefix_1024x24.npz", "dbs_prefix_1024x24_phase.npz", "dbs_prefix_896x24.npz"])
 @pytest.mark.parametrize("mode,refresh", [("psf", 4096), ("psf", 256), ("psf_host", 4096)])
 def test_incremental_greedy_1024x24_equals_oracle(golden_dir, name, mode, refresh):
     """Device walk and host-decided batches: the oracle's accept sequence,
@@ -140,7 +141,7 @@ def test_incremental_greedy_1024x24_16k_equals_oracle(golden_dir, refresh):
     plan.close()
 
 
-@pytest.mark.parametrize("name", ["dbs_prefix_1024x24.npz", "dbs_prefix_1024x24_16k.npz"])
+@pytest.mark.parametrize("name", ["dbs_prefix_1024x24.npz", "dbs_prefix_1024x24_16k.npz", "dbs_prefix_896x24.npz"])
 def test_fft_greedy_1024x24_vs_oracle(golden_dir, name):
     """FFT mode (every candidate a full f32 re-propagation of its group): the
     oracle's accept sequence up to the first candidate whose change lies within
