@@ -547,6 +547,24 @@ class LinearGreedy:
                 break
         return np.array(accepted, bool), np.array(psnrs, np.float64), np.array(deltas, np.float64)
 
+    def run_env(self, actions: Sequence[int]):
+        """The env step's accept / rollback rule over ``actions`` (env.py:184-214: a flip is
+        rolled back iff the PSNR change is negative; the reward 800 * change is returned
+        either way, :188).  Returns (accepted flags, psnr after each flip, change against
+        the previous accepted state).  No termination within the trace (the caller keeps it
+        short of T_PSNR_DIFF)."""
+        accepted, psnrs, deltas = [], [], []
+        for a in actions:
+            ev = self.evaluate(int(a))
+            change = ev[0] - self.previous_psnr                            # env.py:184
+            ok = not (change < 0)                                          # env.py:191
+            if ok:
+                self.commit(int(a), ev)
+            accepted.append(ok)
+            psnrs.append(ev[0])
+            deltas.append(change)
+        return np.array(accepted, bool), np.array(psnrs, np.float64), np.array(deltas, np.float64)
+
 
 def probe_sweep(env: OracleEnv, flips: Sequence[int]):
     """Independent flip-evaluate-undo trials against the fixed base

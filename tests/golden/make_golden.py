@@ -158,6 +158,21 @@ def dbs_prefix_large(cfg, n, seed=0, order_seed=3, stop_diff=None, n_probe=0):
             "probe_delta": probe}
 
 
+def env_trace_large(cfg, n_steps, seed=0, action_seed=2):
+    """The env step (env.py:154-214) at a full reference size: n_steps seeded random
+    actions (rng(2).integers) on the seeded synthetic image, accept iff the
+    PSNR change is >= 0, by the float64 linear evaluator."""
+    pre, tgt = O.synthetic_inputs(cfg, seed)
+    actions = np.random.default_rng(action_seed).integers(0, cfg.channels * cfg.height * cfg.width, n_steps)
+    lg = O.LinearGreedy(cfg, pre, tgt)
+    acc, ps, delta = lg.run_env(actions)
+    return {"seed": np.int64(seed), "action_seed": np.int64(action_seed), "size": np.int64(cfg.height),
+            "groups": np.int64(cfg.groups), "planes": np.int64(cfg.planes),
+            "field_kind": np.int64(cfg.field_kind), "n": np.int64(n_steps), "actions": actions.astype(np.int64),
+            "accepted": acc, "psnr": ps, "delta": delta, "initial_psnr": np.float64(lg.initial_psnr),
+            "final_psnr": np.float64(lg.previous_psnr)}
+
+
 def build_large(only=()):
     """The headline-size fixtures (minutes of CPU; not rebuilt by the CPU tests):
     DBS_1024_24.py greedy prefixes (amplitude 4096 and 16384 candidates, phase 4096) and the
@@ -169,6 +184,8 @@ def build_large(only=()):
         "dbs_ratio05_256.npz": lambda: dbs_prefix_large(O.mono_config(256), None, stop_diff=0.5),
         # the 896 x 896 x 24 crop size (env_1024_24_128.py / DBS_1024_24-128.py), 2,048 candidates
         "dbs_prefix_896x24.npz": lambda: dbs_prefix_large(O.rgb_config(896), 2048, seed=7),
+        # the headline env step (BASELINE configs[2] semantics) over 2,000 random actions
+        "env_trace_1024x24.npz": lambda: env_trace_large(O.rgb_config(1024), 2000),
         # the same amplitude prefix four times longer (~15 min of CPU): its first 4096
         # candidates are dbs_prefix_1024x24.npz's
         "dbs_prefix_1024x24_16k.npz": lambda: dbs_prefix_large(O.rgb_config(1024), 16384),

@@ -13,6 +13,8 @@ re-propagating oracle in tests/test_oracle.py) over
                                 change of the first 512 candidates against the initial state
   dbs_prefix_1024x24_phase.npz  4096 candidates, binary-phase field
   dbs_prefix_896x24.npz         2048 candidates at the 896 x 896 x 24 crop size (seed 7)
+  env_trace_1024x24.npz         2,000 env steps (rng(2) actions) with env.py's rollback rule
+                                (roll back iff change < 0), 1,010 accepts
   dbs_ratio05_256.npz           DBS_ratio_0.5.py's literal run (BASELINE configs[4]):
                                 256x256x8 mono until the PSNR has risen 0.5 dB (:366-372)
 
@@ -38,6 +40,8 @@ from oracle import hbx_oracle as O  # noqa: E402
 
 INCR_TOL_DB = 1e-11     # incremental path vs f64 oracle, per-candidate PSNR change (measured 9.5e-13)
 FFT_TOL_DB = 2e-9       # FFT re-propagation vs f64 oracle, per-candidate PSNR change (measured 1.4e-9)
+ENV_FFT_TOL_DB = 4e-9   # FFT-mode env step: the change is this flip's re-propagated PSNR minus the
+                        # previous accepted flip's, two independent f32 roundoffs (measured 2.5e-9)
 GAIN_TOL_DB = 1e-8      # accumulated PSNR gain of the accepted flips vs the oracle's (measured
                         # 7.5e-11 walk without refresh, 3.7e-9 with exact refreshes every 256
                         # accepts, 7.9e-9 FFT mode)
@@ -283,3 +287,57 @@ def test_walk_mixed_k_fused_and_split_equal_oracle(golden_dir, monkeypatch, refr
     np.bitwise_xor.at(want, (c, r, col), 1)
     assert np.array_equal(mask.cpu().numpy().view("<u8"), O.pack_mask(want))
     plan.close()
+
+
+@pytest.mark.parametrize("mode", ["psf", "fft"])
+def test_env_step_1024x24_trace_vs_oracle(golden_dir, mode):
+    """BASELINE configs[2]'s env step at the headline size over 2,000 seeded random actions
+    (env_trace_1024x24.npz: the float64 oracle with the env's rule -- roll back iff the PSNR
+    change is negative, reward 800 * change either way, env.py:184-214).  The incremental
+    mode makes every decision the oracle's and resolves each change within INCR_TOL_DB; the
+    FFT mode (the reference's algorithm) within ENV_FFT_TOL_DB, its decisions the oracle's
+    until the first step whose change lies inside that bound (measured: all 2,000 steps and
+    1,010 accepts equal in both modes, max change error 1.4e-12 / 2.5e-9 dB)."""
+    import hbx
+    from hbx.env import HologramVecEnv
+    d = np.load(os.path.join(golden_dir, "env_trace_1024x24.npz"), allow_pickle=False)
+    n_px = int(d["size"])
+    ocfg = O.OpticsConfig(n_px, n_px, int(d["groups"]), int(d["planes"]), O.WL_RGB, field_kind=int(d["field_kind"]))
+    pre, tgt = O.synthetic_inputs(ocfg, int(d["seed"]))
+    cfg = hbx.OpticsConfig(n_px, n_px, ocfg.groups, ocfg.planes, tuple(ocfg.wavelengths), field_kind=ocfg.field_kind)
+    pre_t, tgt_t = torch.from_numpy(pre).cuda(), torch.from_numpy(tgt).cuda()
+    env = HologramVecEnv(cfg, 1, lambda i: tgt_t, pre_model_source=lambda i: pre_t, obs_keys=(),
+                         auto_reset=False, mode=mode)
+    env.reset()
+    init = float(env.state.init_psnr[0])
+    assert abs(init - float(d["initial_psnr"])) <= 1e-4
+    acts = torch.from_numpy(d["actions"]).cuda()
+    rs, pss, accs = [], [], []
+    for i in range(len(acts)):
+        r, ps, acc, term, trunc = env.step_device(acts[i:i + 1])
+        rs.append(r.clone()); pss.append(ps.clone()); accs.append(acc.clone())
+    r = torch.cat(rs).cpu().numpy()
+    ps = torch.cat(pss).cpu().numpy()
+    acc = torch.cat(accs).cpu().numpy().astype(bool)
+    want_acc, want_ps, want_delta = d["accepted"], d["psnr"], d["delta"]
+    diff = np.nonzero(acc != want_acc)[0]
+    upto = len(acc) if len(diff) == 0 else int(diff[0])
+    tol = INCR_TOL_DB if mode == "psf" else ENV_FFT_TOL_DB
+    if mode == "psf":
+        assert upto == len(acc), (upto, float(want_delta[upto]))
+    elif upto < len(acc):
+        assert abs(float(want_delta[upto])) <= tol, (upto, float(want_delta[upto]))
+    # the change of every step against the previous accepted state, up to the first divergence
+    prev, change = init, np.empty(upto)
+    for i in range(upto):
+        change[i] = ps[i] - prev
+        if acc[i]:
+            prev = ps[i]
+    err = np.abs(change - want_delta[:upto])
+    print(f"env trace {mode}: {int(acc[:upto].sum())} accepts in {upto} steps, max |change - oracle| "
+          f"{err.max():.2e} dB, max |psnr - oracle| {np.abs(ps[:upto] - want_ps[:upto]).max():.2e} dB")
+    assert err.max() <= tol
+    assert np.abs(r[:upto] - O.RW * want_delta[:upto]).max() <= O.RW * tol
+    assert np.abs(ps[:upto] - want_ps[:upto]).max() <= 1e-4
+    assert upto >= 1000
+    env.close()

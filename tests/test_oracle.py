@@ -297,3 +297,25 @@ def test_long_dbs_prefix_extends_the_4096_fixture(golden_dir):
     assert np.array_equal(a["accepted"], b["accepted"][:n])
     assert np.array_equal(a["psnr"], b["psnr"][:n]) and np.array_equal(a["delta"], b["delta"][:n])
     assert float(a["initial_psnr"]) == float(b["initial_psnr"])
+
+
+def test_env_trace_1024x24_matches_the_stepping_env(golden_dir):
+    """env_trace_1024x24.npz (LinearGreedy.run_env, 2,000 steps) against the
+    re-propagating OracleEnv.step (env.py:154-258) over its first steps: same accept
+    flags, PSNRs and rewards (reward = 800 * change, no terminal bonus inside the trace)."""
+    import os
+    d = np.load(os.path.join(golden_dir, "env_trace_1024x24.npz"), allow_pickle=False)
+    n = int(d["size"])
+    cfg = O.OpticsConfig(n, n, int(d["groups"]), int(d["planes"]), O.WL_RGB, field_kind=int(d["field_kind"]))
+    pre, tgt = O.synthetic_inputs(cfg, int(d["seed"]))
+    acts = np.random.default_rng(int(d["action_seed"])).integers(0, cfg.channels * n * n, int(d["n"]))
+    assert np.array_equal(acts, d["actions"])
+    env = O.OracleEnv(cfg)
+    assert env.reset(pre, tgt) == pytest.approx(float(d["initial_psnr"]), abs=1e-10)
+    for i in range(6):
+        s = env.step(int(acts[i]))
+        assert s.accepted == bool(d["accepted"][i]) and not s.terminated
+        assert s.psnr == pytest.approx(float(d["psnr"][i]), abs=1e-10)
+        assert s.reward == pytest.approx(O.RW * float(d["delta"][i]), abs=1e-8)
+    assert 0.3 < d["accepted"].mean() < 0.7
+    assert float(d["final_psnr"]) - float(d["initial_psnr"]) < 0.1     # stays short of T_PSNR_DIFF
