@@ -213,6 +213,123 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   }
 }
 
+// k_rowfwd at N = 1024 with three workgroups per CU (the wide kernel above: 216 VGPRs,
+// 75.8 KB LDS, two).  The pass is bound by how many row blocks' stores a CU keeps in
+// flight, not by its arithmetic (the whole launch is ~75 us of VALU issue), so:
+//  * lane t loads ONE mask word of its row per plane (word t) and a 32 x 32 bit
+//    transpose across the group (five ds_swizzle levels) hands it bit t of every
+//    word -- the 64 VGPRs of whole-row words the wide kernel keeps for its prefetch
+//    are two here;
+//  * the FFT transposes real and imaginary parts through a 4.2-KB float tile per
+//    group (fft_group_split), and the Hermitian split goes out one plane at a time
+//    through a 32-KB tile that aliases those FFT tiles: 8 KB twiddles + 33.8 KB.
+// Same arithmetic as k_rowfwd, so the A it writes is bit-identical.
+template <int SK>
+__global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__ jobs,
+                                                     const uint32_t* __restrict__ mask,
+                                                     float2* __restrict__ ws_a,
+                                                     const float2* __restrict__ tw_glob, int P, int CH,
+                                                     float va, float vb) {
+  constexpr int R = 32, NT = 256, N = R * R;
+  constexpr int GPB = NT / R;          // 8 rows per row block
+  constexpr int WPR = N / 32;          // 32 mask words per row = one per lane
+  constexpr int RIT = rowfwd_iters<R>();
+  constexpr int SCRF = GPB * R * (R + 1);               // floats: 8 FFT tiles
+  static_assert((N / 2) * GPB * 2 <= SCRF, "one plane's tile must fit in the FFT tiles");
+  __shared__ float2 tw[N];
+  __shared__ __attribute__((aligned(16))) float lds[SCRF];
+
+  for (int i = threadIdx.x; i < N; i += NT) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  const int lane_base = (threadIdx.x & 63) - t;
+  constexpr int RB = N / GPB;
+  constexpr int RBW = RB / RIT;
+  int bid = RIT == 1 ? xcd_pair<RB>(blockIdx.x) : (int)blockIdx.x;
+  const int rbw = bid % RBW;
+  bid /= RBW;
+  const int q = bid % (P / 2);
+  const int j = bid / (P / 2);
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) return;  // uniform per block
+  const int pa = 2 * q, pb = 2 * q + 1;
+  const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
+  uint32_t wa, wb;
+  auto load_row = [&](int y) {
+    wa = plane_a[(size_t)y * WPR + t];
+    wb = plane_a[(size_t)(N + y) * WPR + t];
+  };
+  load_row(rbw * RIT * GPB + grp);
+  __syncthreads();  // tw visible
+
+  constexpr size_t PLA = plane_a_elems(R);
+  float2* base = ws_a + ((size_t)j * P + pa) * PLA;
+  float2* tile = reinterpret_cast<float2*>(lds);
+#pragma unroll 1
+  for (int it = 0; it < RIT; ++it) {
+    const int y0 = (rbw * RIT + it) * GPB;
+    const int y = y0 + grp;
+    // bit r of ta / tb = pixel x = t + 32 r of the row
+    uint32_t ta = group_bit_transpose(wa, t);
+    uint32_t tb = group_bit_transpose(wb, t);
+    if (jb.flip_plane >= 0 && jb.flip_pix / N == y) {  // env.py:164 flip, on the fly
+      const int col = jb.flip_pix % N;
+      if (t == (col & 31)) {
+        if (jb.flip_plane == pa) ta ^= 1u << (col >> 5);
+        if (jb.flip_plane == pb) tb ^= 1u << (col >> 5);
+      }
+    }
+    pk2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj)
+      v[jj] = (pk2){fmaf(vb, (float)((ta >> jj) & 1u), va), fmaf(vb, (float)((tb >> jj) & 1u), va)};
+    if constexpr (RIT > 1) {
+      // next rows' words (the last iteration re-reads its own row: no conditional load)
+      load_row(it + 1 < RIT ? y + GPB : y);
+      if (it > 0) lds_barrier();   // every group has read the previous plane-b tile
+    }
+    fft_group_split<R, false>(v, t, lds + grp * R * (R + 1), tw);
+
+    // Hermitian split: plane a now, plane b kept in registers for the second tile
+    float2 fb[R / 2];
+    lds_barrier();    // every group is done with its FFT tile: reuse as the plane tile
+    const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0
+#pragma unroll
+    for (int k2 = 0; k2 < R / 2; ++k2) {
+      const float2 z = from_pk(v[k2]);
+      const float2 m = mirror_conj<R>(v, k2, t, lane_base);
+      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
+      fb[k2] = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
+        fa = make_float2(z.x, zny.x);
+        fb[k2] = make_float2(z.y, zny.y);
+      }
+      tile[tile_pos<R, GPB>(t + R * k2, grp)] = fa;
+    }
+    constexpr int CHUNKS = (N / 2) * GPB / 2;   // 16-B chunks of one plane's panel
+    static_assert(CHUNKS % NT == 0, "chunking");
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      if (pl == 1) {
+        lds_barrier();   // plane a's tile has been read
+#pragma unroll
+        for (int k2 = 0; k2 < R / 2; ++k2) tile[tile_pos<R, GPB>(t + R * k2, grp)] = fb[k2];
+      }
+      lds_barrier();
+#pragma unroll
+      for (int i = 0; i < CHUNKS / NT; ++i) {
+        const int c = threadIdx.x + NT * i;
+        const int r2 = (c % (GPB / 2)) * 2;
+        const int line = c / (GPB / 2);
+        const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
+        const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
+        st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line, y0 + r2), make_float4(a.x, a.y, b.x, b.y));
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Pass 2
 // ---------------------------------------------------------------------------
@@ -655,6 +772,12 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
     if (tm) tm->begin(0, st);
+#ifndef HBX_ROWFWD_WIDE   // A/B switch: `make exp EXP=ROWFWD_WIDE` keeps the two-block kernel
+    if constexpr (R == 32 && kRowNT<R> == 256)
+      hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
+                         pd.va, pd.vb);
+    else
+#endif
     hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);
     if (tm) tm->end(0, n_jobs, st);
