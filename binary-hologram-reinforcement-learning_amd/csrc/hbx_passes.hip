@@ -499,6 +499,51 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 // ---------------------------------------------------------------------------
 // Pass 3
 // ---------------------------------------------------------------------------
+// k_rowinv's tail: plane mean, f64 partials of (I*T, I^2, T^2) against the target row,
+// fixed-order reduction over the group's lanes and the block's rows.
+template <int R, int GPB>
+__device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, const JobDesc& jb, int j, int y,
+                                                int rb, int grp, int t, const float* __restrict__ target,
+                                                size_t tmask, float* __restrict__ inten_out,
+                                                double* __restrict__ partial, double (&red)[GPB][3]) {
+  constexpr int N = R * R;
+  constexpr int RB = N / GPB;
+  const float invp = 1.0f / (float)P;
+  // tmask = 0 points every row at the plan's zero row (no target): the loads
+  // stay unconditional, so they issue early like the rest of the stream
+  const float* trow = target + ((((size_t)jb.env * G + jb.group) * N + y) * N & tmask);
+  double sxy = 0.0, sxx = 0.0, syy = 0.0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const float I = acc[k] * invp;
+    const float T = trow[t + R * k];
+    sxy = fma((double)I, (double)T, sxy);
+    sxx = fma((double)I, (double)I, sxx);
+    syy = fma((double)T, (double)T, syy);
+    acc[k] = I;
+  }
+  if (inten_out) {
+    float* orow = inten_out + ((size_t)j * N + y) * N;
+#pragma unroll
+    for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
+  }
+  // reduce over the R lanes of the group, fixed order -> bitwise reproducible
+#pragma unroll
+  for (int off = R / 2; off >= 1; off >>= 1) {
+    sxy += __shfl_xor(sxy, off, 64);
+    sxx += __shfl_xor(sxx, off, 64);
+    syy += __shfl_xor(syy, off, 64);
+  }
+  if (t == 0) { red[grp][0] = sxy; red[grp][1] = sxx; red[grp][2] = syy; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, cc = 0.0;
+    for (int g = 0; g < GPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
+    double* o = partial + ((size_t)j * RB + rb) * 3;
+    o[0] = a; o[1] = b; o[2] = cc;
+  }
+}
+
 template <int R, int NT>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restrict__ jobs,
                                                    const float2* __restrict__ ws_b,
@@ -584,40 +629,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
     }
   }
 
-  const float invp = 1.0f / (float)P;
-  // tmask = 0 points every row at the plan's zero row (no target): the loads
-  // stay unconditional, so they issue early like the rest of the stream
-  const float* trow = target + ((((size_t)jb.env * G + jb.group) * N + y) * N & tmask);
-  double sxy = 0.0, sxx = 0.0, syy = 0.0;
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    const float I = acc[k] * invp;
-    const float T = trow[t + R * k];
-    sxy = fma((double)I, (double)T, sxy);
-    sxx = fma((double)I, (double)I, sxx);
-    syy = fma((double)T, (double)T, syy);
-    acc[k] = I;
-  }
-  if (inten_out) {
-    float* orow = inten_out + ((size_t)j * N + y) * N;
-#pragma unroll
-    for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
-  }
-  // reduce over the R lanes of the group, fixed order -> bitwise reproducible
-#pragma unroll
-  for (int off = R / 2; off >= 1; off >>= 1) {
-    sxy += __shfl_xor(sxy, off, 64);
-    sxx += __shfl_xor(sxx, off, 64);
-    syy += __shfl_xor(syy, off, 64);
-  }
-  if (t == 0) { red[grp][0] = sxy; red[grp][1] = sxx; red[grp][2] = syy; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0, cc = 0.0;
-    for (int g = 0; g < GPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
-    double* o = partial + ((size_t)j * RB + rb) * 3;
-    o[0] = a; o[1] = b; o[2] = cc;
-  }
+  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, partial, red);
 }
 
 // ---------------------------------------------------------------------------
