@@ -333,17 +333,27 @@ __device__ __forceinline__ void fft_group(T (&v)[R], int t, const Scratch& sc, c
 // R = 32 instead of 8.4 KB).  Same result, bit for bit: only the LDS hand-off
 // differs.  Each half of v is overwritten only after the whole group has
 // written it out (wave_sync), so no extra registers are held.
-template <int R, bool INV>
-__device__ __forceinline__ void fft_group_split(pk2 (&v)[R], int t, float* sc, const float2* tw) {
+template <int R, bool INV, bool SCALAR = false, class T>
+__device__ __forceinline__ void fft_group_split(T (&v)[R], int t, float* sc, const float2* tw) {
   asm volatile("" ::: "memory");
 #ifdef HBX_NO_FFT
   return;
 #endif
-  dft_reg<R, INV>(v);
+  if constexpr (SCALAR) {
+    static_assert(std::is_same<T, float2>::value, "scalar FFT works on float2");
+    dft_reg_scalar<R, INV>(v);
 #pragma unroll
-  for (int k1 = 1; k1 < R; ++k1) {
-    const pk2 w = to_pk(tw[k1 * R + t]);
-    v[k1] = INV ? pk_cmulc(v[k1], w) : pk_cmul(v[k1], w);
+    for (int k1 = 1; k1 < R; ++k1) {
+      const float2 w = tw[k1 * R + t];
+      v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    }
+  } else {
+    dft_reg<R, INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) {
+      const pk2 w = to_pk(tw[k1 * R + t]);
+      v[k1] = st_pk<T>(INV ? pk_cmulc(ld_pk(v[k1]), w) : pk_cmul(ld_pk(v[k1]), w));
+    }
   }
   wave_sync();  // previous users of the scratch are done
 #pragma unroll
@@ -358,13 +368,10 @@ __device__ __forceinline__ void fft_group_split(pk2 (&v)[R], int t, float* sc, c
 #pragma unroll
   for (int tt = 0; tt < R; ++tt) v[tt].y = sc[tt * (R + 1) + t];
   wave_sync();
-  dft_reg<R, INV>(v);
+  if constexpr (SCALAR) dft_reg_scalar<R, INV>(v);
+  else dft_reg<R, INV>(v);
 }
 
-// 32 x 32 bit-matrix transpose across the 32 lanes of a group: lane t holds
-// word A[t] and gets B[t] with bit r of B[t] = bit t of A[r].  Five butterfly
-// levels, each one ds_swizzle (xor of the lane index, inside 32 lanes) and the
-// block swap of the off-diagonal j x j bit blocks.
 template <int J>
 __device__ __forceinline__ uint32_t bit_transpose_level(uint32_t x, int t) {
   constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
