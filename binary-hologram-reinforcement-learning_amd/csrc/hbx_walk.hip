@@ -479,6 +479,15 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   // per quad: every load (pending commits, then each candidate's plane / intensity /
   // target / shifted single-pixel field) is issued before any arithmetic or store, so a
   // quad costs one memory round trip; values a commit produces replace the loaded ones
+#ifdef HBX_WALK_NT   // timing experiment: non-temporal plane / intensity / target loads
+  auto ld4 = [](const float4* p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  };
+#else
+  auto ld4 = [](const float4* p) { return *p; };
+#endif
   for (int q = blockIdx.x * kWalkNT + threadIdx.x; q < nq; q += gridDim.x * kWalkNT) {
     const int y = (4 * q) / N, x0 = (4 * q) % N;
     float cu[2][8], ci[2][4], chh[2][8];
@@ -487,10 +496,10 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     for (int c = 0; c < 2; ++c) {
       if (c >= nc) break;
       const float4* U = reinterpret_cast<const float4*>(a.field + (size_t)cm[c].ch * hw);
-      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+      const float4 u01 = ld4(U + 2 * q), u23 = ld4(U + 2 * q + 1);
       cu[c][0] = u01.x; cu[c][1] = u01.y; cu[c][2] = u01.z; cu[c][3] = u01.w;
       cu[c][4] = u23.x; cu[c][5] = u23.y; cu[c][6] = u23.z; cu[c][7] = u23.w;
-      const float4 iv = reinterpret_cast<const float4*>(a.inten + (size_t)cm[c].g * hw)[q];
+      const float4 iv = ld4(reinterpret_cast<const float4*>(a.inten + (size_t)cm[c].g * hw) + q);
       ci[c][0] = iv.x; ci[c][1] = iv.y; ci[c][2] = iv.z; ci[c][3] = iv.w;
       const float2* hrow = a.hpsf + (size_t)cm[c].g * hw + (size_t)wfold(y - cm[c].r, N) * N;
 #pragma unroll
@@ -504,12 +513,12 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     for (int j = 0; j < K; ++j) {
       if (j >= kv || !cd[j].ok) continue;
       const float4* U = reinterpret_cast<const float4*>(a.field + (size_t)cd[j].ch * hw);
-      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
+      const float4 u01 = ld4(U + 2 * q), u23 = ld4(U + 2 * q + 1);
       lu[j][0] = u01.x; lu[j][1] = u01.y; lu[j][2] = u01.z; lu[j][3] = u01.w;
       lu[j][4] = u23.x; lu[j][5] = u23.y; lu[j][6] = u23.z; lu[j][7] = u23.w;
-      const float4 iv = reinterpret_cast<const float4*>(a.inten + (size_t)cd[j].g * hw)[q];
+      const float4 iv = ld4(reinterpret_cast<const float4*>(a.inten + (size_t)cd[j].g * hw) + q);
       li[j][0] = iv.x; li[j][1] = iv.y; li[j][2] = iv.z; li[j][3] = iv.w;
-      const float4 tv = reinterpret_cast<const float4*>(a.target + (size_t)cd[j].g * hw)[q];
+      const float4 tv = ld4(reinterpret_cast<const float4*>(a.target + (size_t)cd[j].g * hw) + q);
       lt[j][0] = tv.x; lt[j][1] = tv.y; lt[j][2] = tv.z; lt[j][3] = tv.w;
       const float2* hrow = a.hpsf + (size_t)cd[j].g * hw + (size_t)wfold(y - cd[j].r, N) * N;
 #pragma unroll
