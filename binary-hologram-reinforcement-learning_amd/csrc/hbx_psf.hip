@@ -192,17 +192,8 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
   const int nq = (int)(hw / 4);
   for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
     const int y = (4 * q) / N, x0 = (4 * q) % N;
-#ifdef HBX_PSF_COMMIT_NT
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v a = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(U + 2 * q));
-    const f4v b = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(U + 2 * q + 1));
-    const f4v c = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(I + q));
-    float4 u01 = make_float4(a.x, a.y, a.z, a.w), u23 = make_float4(b.x, b.y, b.z, b.w);
-    float4 iv = make_float4(c.x, c.y, c.z, c.w);
-#else
     float4 u01 = U[2 * q], u23 = U[2 * q + 1];
     float4 iv = I[q];
-#endif
     const float2* hrow = h + (size_t)fold(y - r, N) * N;
     const float2 h0 = hrow[fold(x0 - col, N)], h1 = hrow[fold(x0 + 1 - col, N)];
     const float2 h2 = hrow[fold(x0 + 2 - col, N)], h3 = hrow[fold(x0 + 3 - col, N)];
@@ -216,15 +207,9 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
       uu[2 * k] = fmaf(delta, hh[2 * k], ur);
       uu[2 * k + 1] = fmaf(delta, hh[2 * k + 1], ui);
     }
-#ifdef HBX_PSF_COMMIT_NT
-    __builtin_nontemporal_store((f4v){uu[0], uu[1], uu[2], uu[3]}, reinterpret_cast<f4v*>(U + 2 * q));
-    __builtin_nontemporal_store((f4v){uu[4], uu[5], uu[6], uu[7]}, reinterpret_cast<f4v*>(U + 2 * q + 1));
-    __builtin_nontemporal_store((f4v){ii[0], ii[1], ii[2], ii[3]}, reinterpret_cast<f4v*>(I + q));
-#else
     U[2 * q] = make_float4(uu[0], uu[1], uu[2], uu[3]);
     U[2 * q + 1] = make_float4(uu[4], uu[5], uu[6], uu[7]);
     I[q] = make_float4(ii[0], ii[1], ii[2], ii[3]);
-#endif
   }
 }
 

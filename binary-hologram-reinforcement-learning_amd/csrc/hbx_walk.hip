@@ -479,15 +479,8 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   // per quad: every load (pending commits, then each candidate's plane / intensity /
   // target / shifted single-pixel field) is issued before any arithmetic or store, so a
   // quad costs one memory round trip; values a commit produces replace the loaded ones
-#ifdef HBX_WALK_NT   // timing experiment: non-temporal plane / intensity / target loads
-  auto ld4 = [](const float4* p) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-  };
-#else
-  auto ld4 = [](const float4* p) { return *p; };
-#endif
+  auto ld4 = [](const float4* p) { return *p; };   // (non-temporal loads measured slower: the
+  // working set of a sweep, 24 planes + 3 intensities + 3 targets = 216 MB, lives in the MALL)
   for (int q = blockIdx.x * kWalkNT + threadIdx.x; q < nq; q += gridDim.x * kWalkNT) {
     const int y = (4 * q) / N, x0 = (4 * q) % N;
     float cu[2][8], ci[2][4], chh[2][8];
