@@ -370,8 +370,24 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? HBX_COL2_ITER : (R == 16 ? 2 : 1); }
 
+// Second output line without the LDS mirror (default; HBX_COL2_MIRROR keeps the
+// round-1 hand-off for A/B runs): H is even in ky, so
+//   IFFT_y(M H)(y) = conj IFFT_y(Z conj H)(y),   M(ky) = conj Z(-ky),
+// i.e. B line N - kx is the conjugate of the inverse FFT of W = Z conj H, which
+// the lanes form in registers from the same H values as Z H.  Only kx = 0 still
+// needs M itself ((Z + M)/2 and (Z - M)/2 are the transforms of the two real
+// lines packed into A line 0): a register shuffle, mirror_conj.
+// HBX_COL2_WPB = 3 builds the pass for three workgroups per CU: float transpose
+// tiles (fft_group_split, 4.2 KB per group) and no next-line prefetch (the
+// third workgroup hides the line loads instead).
+#ifndef HBX_COL2_WPB
+#define HBX_COL2_WPB 2
+#endif
+#ifndef HBX_COL2_PREFETCH
+#define HBX_COL2_PREFETCH (HBX_COL2_WPB < 3)
+#endif
 template <int R, int SK>
-__global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
+__global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __restrict__ jobs,
                                                  const float2* __restrict__ ws_a,
                                                  float2* __restrict__ ws_b,
                                                  const float2* __restrict__ htab,
@@ -382,12 +398,23 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   constexpr int LB = (N / 2) / (GPB * ITER);
   static_assert((N / 2) % (GPB * ITER) == 0, "line blocking");
   __shared__ float2 tw[N];
-  __shared__ float2 scratch[GPB * R * (R + 1)];
 
   for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
+#if HBX_COL2_WPB > 2
+  __shared__ float scratch[GPB * R * (R + 1)];
+  float* const scf = scratch + grp * R * (R + 1);
+#define COL2_FFT(arr, INV) fft_group_split<R, INV, HBX_COL2_SCALAR>(arr, t, scf, tw)
+#else
+  __shared__ float2 scratch[GPB * R * (R + 1)];
+#define COL2_FFT(arr, INV) fft_group<R, INV, HBX_COL2_SCALAR>(arr, t, sc, tw)
+#endif
+#ifndef HBX_COL2_MIRROR
+  static_assert(HBX_COL2_SCALAR, "the conjugate form keeps the scalar DFT");
+  const int lane_base = (threadIdx.x & 63) - t;
+#endif
   int bid = blockIdx.x;
   const int lb = bid % LB;
   bid /= LB;
@@ -401,8 +428,13 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
   // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
+#if HBX_COL2_WPB <= 2
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+#endif
+#ifdef HBX_COL2_MIRROR
+  static_assert(HBX_COL2_WPB <= 2, "the LDS mirror needs the complex scratch");
   const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
+#endif
   // the LB blocks of a plane run side by side: at iteration it they hold lines
   // it * LB * GPB + [0, LB * GPB), i.e. whole contiguous stretches of every panel
   constexpr int KSTEP = LB * GPB;
@@ -431,6 +463,62 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 #else
 #define COL2_H(k2) buf_ld2(rh, vh, (k2) * R * 8)
 #endif
+#ifndef HBX_COL2_MIRROR
+    COL2_FFT(v, false);
+    COL2_T w[R];
+    if (!dc) {   // v <- Z H, w <- Z conj H, each H value consumed as it arrives
+#pragma unroll
+      for (int c8 = 0; c8 < R; c8 += 8) {
+        float2 hb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) hb[i] = COL2_H(c8 + i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          w[c8 + i] = COL2_CMULC(v[c8 + i], hb[i]);
+          v[c8 + i] = COL2_CMUL(v[c8 + i], hb[i]);
+        }
+      }
+    } else {     // kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
+      const int vn = ((N / 2) * N + t) * 8;
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) w[k2] = mirror_conj<R>(v, k2, t, lane_base);
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) {
+        const float2 z = v[k2], mm = w[k2];
+        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), COL2_H(k2));
+        w[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * R * 8));
+      }
+    }
+    COL2_FFT(v, true);
+    {
+      const int vo = PB::voff(t, kx);
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(v[k2]), rb, vo, PB::joff(k2));
+    }
+#if HBX_COL2_PREFETCH
+    if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
+      const int vo = PA::voff(t, kx + KSTEP);
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
+    }
+#endif
+    COL2_FFT(w, true);
+    {
+      const int vo = PB::voff(t, dc ? N / 2 : N - kx);
+      const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2)
+        buf_st2s(store_round<SK>(make_float2(w[k2].x, sy * w[k2].y)), rb, vo, PB::joff(k2));
+    }
+#if !HBX_COL2_PREFETCH
+    if (it + 1 < ITER) {
+      const int vo = PA::voff(t, kx + KSTEP);
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
+    }
+#endif
+  }
+#else   // HBX_COL2_MIRROR: round-1 form, W through the group's scratch
 #ifdef HBX_COL2_FWD_PACKED   // A/B switch: packed DFTs for the forward FFT only (one line live)
     fft_group<R, false, false>(v, t, sc, tw);
 #else
@@ -493,7 +581,9 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
     }
   }
+#endif
 #undef COL2_H
+#undef COL2_FFT
 }
 
 // ---------------------------------------------------------------------------
