@@ -334,14 +334,14 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 // Pass 2
 // ---------------------------------------------------------------------------
 // Column pass, one lane group per input line and both of its output lines:
-// forward FFT over y -> Z; Z into the group's scratch, M = conj Z(-ky) read
-// back into registers; both multiplied by the same H(kx, .) row (H is even
-// in fx); inverse FFT of Z H -> B line kx, then of M H -> B line N - kx
-// (kx = 0: (Z + M)/2 -> line 0 and -i (Z - M)/2 with the H(N/2) row -> line
-// N/2).  One forward FFT per input line instead of one per output line (the
-// two-role k_col), one A read, one H read, and no cross-group traffic: every
-// LDS hand-off stays inside the group's own scratch (wave_sync only).  The
-// next line's loads go into v as soon as line kx is stored and fly under the
+// forward FFT over y -> Z; Z H and Z conj H from the same H(kx, .) row (H is
+// even in fx and fy); inverse FFT of Z H -> B line kx, conjugate of the
+// inverse FFT of Z conj H -> B line N - kx (kx = 0: (Z + M)/2 -> line 0 and
+// -i (Z - M)/2 with the H(N/2) row -> line N/2, M = conj Z(-ky)).  One
+// forward FFT per input line instead of one per output line (the two-role
+// k_col), one A read, one H read, and no cross-group traffic: every LDS
+// hand-off stays inside the group's own scratch (wave_sync only).  The next
+// line's loads go into v as soon as line kx is stored and fly under the
 // second inverse FFT.  Scalar-f32 FFTs here: with two lines in registers the
 // packed variant (hbx_fft.hpp) spills.
 #ifndef HBX_COL2_SCALAR
