@@ -134,7 +134,7 @@ hipError_t run_jobs_generic(const PlanDev& pd, const JobDesc* jobs, int n_jobs, 
   hipLaunchKernelGGL(k_gen_reduce, dim3((unsigned)(n_jobs * RB)), dim3(256), 0, st, jobs, X, target, N, P,
                      pd.G, pd.partial, inten_out, field_out);
   if (tm) tm->end(2, n_jobs, st);
-  hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial, n_jobs, RB,
+  hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial, n_jobs, RB,
                      pd.job_stats);
   return hipGetLastError();
 }

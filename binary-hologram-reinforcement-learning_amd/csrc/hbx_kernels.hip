@@ -85,14 +85,27 @@ __global__ void k_jobs_full(const int32_t* __restrict__ env_ids, int n_ids, int 
 }
 
 // sum the row-block partials of every job (fixed order) -> job_stats[j][3]
-__global__ void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,
-                                  double* __restrict__ job_stats) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// grid (n_jobs), one wave per job: the wave stages the job's row-block partials in LDS with
+// coalesced loads, then lane 0 adds them in row-block order (the fixed order every result
+// depends on, bit for bit).  One thread per job walking its 3 KB of partials took ~20 us
+// per 128-job launch (rocprofv3, profiles/r02_final4/kernel_stats.csv).
+__global__ __launch_bounds__(64) void k_reduce_partials(const double* __restrict__ partial, int n_jobs, int RB,
+                                                        double* __restrict__ job_stats) {
+  constexpr int CHUNK = 768;   // doubles per staging round (a multiple of 3)
+  __shared__ double s[CHUNK];
+  const int j = blockIdx.x;
   if (j >= n_jobs) return;
   double a = 0.0, b = 0.0, c = 0.0;
   const double* p = partial + (size_t)j * RB * 3;
-  for (int r = 0; r < RB; ++r) { a += p[3 * r]; b += p[3 * r + 1]; c += p[3 * r + 2]; }
-  job_stats[3 * j] = a; job_stats[3 * j + 1] = b; job_stats[3 * j + 2] = c;
+  for (int c0 = 0; c0 < 3 * RB; c0 += CHUNK) {
+    const int n = 3 * RB - c0 < CHUNK ? 3 * RB - c0 : CHUNK;
+    for (int i = threadIdx.x; i < n; i += 64) s[i] = p[c0 + i];
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < n; i += 3) { a += s[i]; b += s[i + 1]; c += s[i + 2]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { job_stats[3 * j] = a; job_stats[3 * j + 1] = b; job_stats[3 * j + 2] = c; }
 }
 
 // scatter full-propagation job stats into chan_stats[env][g]; psnr per env

@@ -425,7 +425,7 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
                      target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
                      target ? ~(size_t)0 : (size_t)0);
   if (tm) tm->end(2, n_jobs, st);
-  hipLaunchKernelGGL(k_reduce_partials, dim3((n_jobs + 63) / 64), dim3(64), 0, st, pd.partial, n_jobs, kRB,
+  hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial, n_jobs, kRB,
                      pd.job_stats);
   return hipGetLastError();
 }

@@ -59,17 +59,52 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double (*red)[2
 
 }  // namespace
 
-// stable counting sort of the jobs by colour group (single block): launches
-// then visit one group's jobs after another, so h_g stays L2-resident
-__global__ void k_psf_order(const JobDesc* __restrict__ jobs, int n_jobs, int G,
-                            int32_t* __restrict__ order) {
+// stable counting sort of the jobs by colour group (one block of 256 threads):
+// launches then visit one group's jobs after another, so h_g stays L2-resident.
+// Job j goes to (jobs of smaller groups) + (jobs of its group before it), both
+// from per-wave ballots over chunks of 256 jobs -- the order of the serial
+// sort, without its 2 * n_jobs dependent loads (34 us per 128-job step as one
+// thread, rocprofv3 profiles/r02_final4/kernel_stats.csv).  Jobs without an env
+// count as group 0, as before.
+__global__ __launch_bounds__(256) void k_psf_order(const JobDesc* __restrict__ jobs, int n_jobs, int G,
+                                                   int32_t* __restrict__ order) {
+  constexpr int W = 256 / 64;
+  __shared__ int wc[W][8];   // this chunk's jobs per wave and group
+  __shared__ int run[8];     // jobs per group in the chunks before this one
   __shared__ int base[8];
-  if (threadIdx.x == 0) {
-    int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < n_jobs; ++j) cnt[jobs[j].env >= 0 ? jobs[j].group : 0]++;
-    int acc = 0;
-    for (int g = 0; g < G; ++g) { base[g] = acc; acc += cnt[g]; }
-    for (int j = 0; j < n_jobs; ++j) order[base[jobs[j].env >= 0 ? jobs[j].group : 0]++] = j;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (threadIdx.x < 8) run[threadIdx.x] = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < n_jobs; c0 += 256) {
+      const int j = c0 + (int)threadIdx.x;
+      const int g = j < n_jobs ? (jobs[j].env >= 0 ? jobs[j].group : 0) : -1;
+      int mine = 0;
+      for (int gg = 0; gg < G; ++gg) {
+        const uint64_t m = __ballot(g == gg);
+        if (lane == 0) wc[w][gg] = __popcll(m);
+        if (g == gg) mine = __popcll(m & below);
+      }
+      __syncthreads();
+      if (pass == 1 && g >= 0) {
+        int pos = base[g] + run[g] + mine;
+        for (int ww = 0; ww < w; ++ww) pos += wc[ww][g];
+        order[pos] = j;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < G) {
+        int s = 0;
+        for (int ww = 0; ww < W; ++ww) s += wc[ww][threadIdx.x];
+        run[threadIdx.x] += s;
+      }
+      __syncthreads();
+    }
+    if (pass == 0 && threadIdx.x == 0) {
+      int acc = 0;
+      for (int gg = 0; gg < G; ++gg) { base[gg] = acc; acc += run[gg]; }
+    }
+    __syncthreads();
   }
 }
 
@@ -148,15 +183,21 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
 // fixed-order reduction of the block partials (the flip's increments of sum IT
 // and sum I^2) added to the cached channel statistics; sum T^2 of the touched
 // channel is unchanged by a flip
-__global__ void k_psf_reduce(const JobDesc* __restrict__ jobs, const double* __restrict__ partial,
-                             int n_jobs, int G, const double* __restrict__ chan_stats,
-                             double* __restrict__ job_stats) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// grid (n_jobs), one wave per job: coalesced staging of the block partials in LDS, then
+// lane 0 adds them in block order (as k_reduce_partials)
+__global__ __launch_bounds__(64) void k_psf_reduce(const JobDesc* __restrict__ jobs, const double* __restrict__ partial,
+                                                   int n_jobs, int G, const double* __restrict__ chan_stats,
+                                                   double* __restrict__ job_stats) {
+  __shared__ double s[2 * kPsfBlocks];
+  const int j = blockIdx.x;
   if (j >= n_jobs) return;
+  const double* p = partial + (size_t)j * kPsfBlocks * 2;
+  for (int i = threadIdx.x; i < 2 * kPsfBlocks; i += 64) s[i] = p[i];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const JobDesc jb = jobs[j];
   double a = 0.0, b = 0.0;
-  const double* p = partial + (size_t)j * kPsfBlocks * 2;
-  for (int i = 0; i < kPsfBlocks; ++i) { a += p[2 * i]; b += p[2 * i + 1]; }
+  for (int i = 0; i < kPsfBlocks; ++i) { a += s[2 * i]; b += s[2 * i + 1]; }
   if (jb.env < 0) {
     job_stats[3 * j] = job_stats[3 * j + 1] = job_stats[3 * j + 2] = 0.0;
     return;
@@ -217,12 +258,12 @@ hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, c
                            const float2* field, const float* inten, const float* target,
                            const double* chan_stats, hipStream_t st) {
   PassTimer* tm = pd.timer;
-  hipLaunchKernelGGL(k_psf_order, dim3(1), dim3(64), 0, st, jobs, n_jobs, pd.G, pd.psf_order);
+  hipLaunchKernelGGL(k_psf_order, dim3(1), dim3(256), 0, st, jobs, n_jobs, pd.G, pd.psf_order);
   if (tm) tm->begin(3, st);
   hipLaunchKernelGGL(k_psf_eval, dim3(kPsfBlocks, n_jobs), dim3(256), 0, st, jobs, pd.psf_order, mask, field, inten,
                      target, pd.hpsf, pd.N, pd.P, pd.G, pd.vb, pd.psf_partial);
   if (tm) tm->end(3, n_jobs, st);
-  hipLaunchKernelGGL(k_psf_reduce, dim3((n_jobs + 63) / 64), dim3(64), 0, st, jobs, pd.psf_partial,
+  hipLaunchKernelGGL(k_psf_reduce, dim3(n_jobs), dim3(64), 0, st, jobs, pd.psf_partial,
                      n_jobs, pd.G, chan_stats, pd.job_stats);
   return hipGetLastError();
 }
