@@ -95,17 +95,20 @@ __global__ __launch_bounds__(64) void k_reduce_partials(const double* __restrict
   __shared__ double s[CHUNK];
   const int j = blockIdx.x;
   if (j >= n_jobs) return;
-  double a = 0.0, b = 0.0, c = 0.0;
+  // lane k < 3 carries sum k (a separate chain per statistic, each in row-block order)
+  const int k = threadIdx.x;
+  double acc = 0.0;
   const double* p = partial + (size_t)j * RB * 3;
   for (int c0 = 0; c0 < 3 * RB; c0 += CHUNK) {
     const int n = 3 * RB - c0 < CHUNK ? 3 * RB - c0 : CHUNK;
     for (int i = threadIdx.x; i < n; i += 64) s[i] = p[c0 + i];
     __syncthreads();
-    if (threadIdx.x == 0)
-      for (int i = 0; i < n; i += 3) { a += s[i]; b += s[i + 1]; c += s[i + 2]; }
+    if (k < 3)
+#pragma unroll 8
+      for (int i = k; i < n; i += 3) acc += s[i];
     __syncthreads();
   }
-  if (threadIdx.x == 0) { job_stats[3 * j] = a; job_stats[3 * j + 1] = b; job_stats[3 * j + 2] = c; }
+  if (k < 3) job_stats[3 * j + k] = acc;
 }
 
 // scatter full-propagation job stats into chan_stats[env][g]; psnr per env

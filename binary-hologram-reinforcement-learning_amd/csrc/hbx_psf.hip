@@ -194,10 +194,16 @@ __global__ __launch_bounds__(64) void k_psf_reduce(const JobDesc* __restrict__ j
   const double* p = partial + (size_t)j * kPsfBlocks * 2;
   for (int i = threadIdx.x; i < 2 * kPsfBlocks; i += 64) s[i] = p[i];
   __syncthreads();
+  // lanes 0 and 1 carry the two sums, each in block order; lane 0 then writes both
+  double acc = 0.0;
+  if (threadIdx.x < 2) {
+#pragma unroll 8
+    for (int i = threadIdx.x; i < 2 * kPsfBlocks; i += 2) acc += s[i];
+  }
+  const double b = __shfl(acc, 1, 64);
   if (threadIdx.x != 0) return;
+  const double a = acc;
   const JobDesc jb = jobs[j];
-  double a = 0.0, b = 0.0;
-  for (int i = 0; i < kPsfBlocks; ++i) { a += s[2 * i]; b += s[2 * i + 1]; }
   if (jb.env < 0) {
     job_stats[3 * j] = job_stats[3 * j + 1] = job_stats[3 * j + 2] = 0.0;
     return;

@@ -479,6 +479,35 @@ def test_psf_matches_fft_full_size(field_kind):
     psf.close()
 
 
+def test_psf_matches_fft_many_envs():
+    """300 envs at 64 x 64 x (3 x 2): more jobs than one 256-job chunk of k_psf_order's
+    ballot sort (hbx_psf.hip), all three colour groups mixed in every step; the
+    incremental and FFT modes agree step by step (PSNR, accept flags) and end on the
+    same masks."""
+    from hbx.env import HologramVecEnv
+    cfg = dev_cfg(small_rgb())
+    B = 300
+    g = torch.Generator(device="cuda").manual_seed(7)
+    pres = torch.rand((B, 6, 64, 64), generator=g, device="cuda")
+    tgts = torch.rand((B, 3, 64, 64), generator=g, device="cuda")
+    kw = dict(pre_model_source=lambda i: pres[i], obs_keys=(), auto_reset=False)
+    fft = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    psf = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="psf", refresh_every=8, **kw)
+    fft.reset()
+    psf.reset()
+    acts = torch.randint(0, 6 * 64 * 64, (12, B), generator=g, device="cuda")
+    for k in range(12):
+        prev = fft.state.prev_psnr.clone()
+        _, p1, a1, _, _ = fft.step_device(acts[k])
+        _, p2, a2, _, _ = psf.step_device(acts[k])
+        assert torch.max(torch.abs(p1 - p2)).item() <= PSNR_TOL
+        differ = a1 != a2
+        assert bool((torch.abs(p1 - prev)[differ] < 1e-5).all()), f"step {k}: decisions differ"
+    assert torch.equal(fft.state.mask, psf.state.mask)
+    fft.close()
+    psf.close()
+
+
 # ---------------------------------------------------------------------------
 # all-flip PSNR-change map (hbx_flip_map, correlation evaluation)
 # ---------------------------------------------------------------------------
