@@ -548,8 +548,9 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
     const EnvDev ed = env_offset(base, b0, CH, G, N);
     float2* fld = reinterpret_cast<float2*>(e->field) + (size_t)b0 * CH * hw;
     float* inten = e->intensity + (size_t)b0 * G * hw;
-    HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
-    HBX_HIP(hbx::launch_psf_eval(pd, p->jobs, n, ed.mask, fld, inten, ed.target, ed.chan_stats, st));
+    // the job decode rides in k_psf_order's launch (actions -> jobs, then the colour sort)
+    HBX_HIP(hbx::launch_psf_eval(pd, p->jobs, n, ed.mask, fld, inten, ed.target, ed.chan_stats, st, actions + b0,
+                                 e->error ? e->error : p->err));
     HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),
                                           p->optics.rel_scale, p->optics.peak,
                                           reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,

@@ -205,7 +205,8 @@ hipError_t map_group(const PlanDev& pd, int g, const float2* field, const float*
                      double peak, hipStream_t st);
 hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                            const float2* field, const float* inten, const float* target,
-                           const double* chan_stats, hipStream_t st);
+                           const double* chan_stats, hipStream_t st, const int64_t* actions = nullptr,
+                           int32_t* err = nullptr);
 // device-resident greedy DBS walk (hbx_walk.hip)
 struct WalkLaunch {
   uint64_t* mask;

@@ -66,8 +66,11 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double (*red)[2
 // sort, without its 2 * n_jobs dependent loads (34 us per 128-job step as one
 // thread, rocprofv3 profiles/r02_final4/kernel_stats.csv).  Jobs without an env
 // count as group 0, as before.
-__global__ __launch_bounds__(256) void k_psf_order(const JobDesc* __restrict__ jobs, int n_jobs, int G,
-                                                   int32_t* __restrict__ order) {
+// With actions != nullptr the same launch first decodes the env-step actions into the
+// jobs (k_jobs_from_actions' rule, env.py:157-161), saving the env step one launch.
+__global__ __launch_bounds__(256) void k_psf_order(JobDesc* __restrict__ jobs, int n_jobs, int G,
+                                                   int32_t* __restrict__ order, const int64_t* __restrict__ actions,
+                                                   int N, int P, int32_t* __restrict__ err) {
   constexpr int W = 256 / 64;
   __shared__ int wc[W][8];   // this chunk's jobs per wave and group
   __shared__ int run[8];     // jobs per group in the chunks before this one
@@ -79,7 +82,25 @@ __global__ __launch_bounds__(256) void k_psf_order(const JobDesc* __restrict__ j
     __syncthreads();
     for (int c0 = 0; c0 < n_jobs; c0 += 256) {
       const int j = c0 + (int)threadIdx.x;
-      const int g = j < n_jobs ? (jobs[j].env >= 0 ? jobs[j].group : 0) : -1;
+      int g = -1;
+      if (j < n_jobs) {
+        if (actions) {   // decode (both passes: registers only; the jobs are written once)
+          const int64_t a = actions[j];
+          const int64_t hw = (int64_t)N * N;
+          JobDesc jd;
+          if (a < 0 || a >= (int64_t)G * P * hw) {
+            jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
+            if (pass == 0 && err) atomicOr(err, 1);
+          } else {
+            const int ch = (int)(a / hw);
+            jd.env = j; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(a % hw);
+          }
+          if (pass == 0) jobs[j] = jd;
+          g = jd.group;
+        } else {
+          g = jobs[j].env >= 0 ? jobs[j].group : 0;
+        }
+      }
       int mine = 0;
       for (int gg = 0; gg < G; ++gg) {
         const uint64_t m = __ballot(g == gg);
@@ -236,6 +257,23 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
   float4* U = reinterpret_cast<float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
   float4* I = reinterpret_cast<float4*>(inten + ((size_t)jb.env * G + g) * hw);
   const float2* h = hpsf + (size_t)g * hw;
+#ifdef HBX_PSF_COMMIT_PX1   // A/B switch: one pixel per lane, as k_psf_eval (coalesced shifted-h reads)
+  float2* U2 = reinterpret_cast<float2*>(U);
+  float* I1 = reinterpret_cast<float*>(I);
+#pragma unroll 4
+  for (int q = blockIdx.x * 256 + threadIdx.x; q < (int)hw; q += kPsfBlocks * 256) {
+    const int y = q / N, x = q % N;
+    float2 u = U2[q];
+    float iv = I1[q];
+    const float2 hv = h[(size_t)fold(y - r, N) * N + fold(x - col, N)];
+    iv += flip_dI(u.x, u.y, hv.x, hv.y, delta, invp);
+    u.x = fmaf(delta, hv.x, u.x);
+    u.y = fmaf(delta, hv.y, u.y);
+    U2[q] = u;
+    I1[q] = iv;
+  }
+  return;
+#endif
   const int nq = (int)(hw / 4);
   for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
     const int y = (4 * q) / N, x0 = (4 * q) % N;
@@ -262,9 +300,10 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
 
 hipError_t launch_psf_eval(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
                            const float2* field, const float* inten, const float* target,
-                           const double* chan_stats, hipStream_t st) {
+                           const double* chan_stats, hipStream_t st, const int64_t* actions, int32_t* err) {
   PassTimer* tm = pd.timer;
-  hipLaunchKernelGGL(k_psf_order, dim3(1), dim3(256), 0, st, jobs, n_jobs, pd.G, pd.psf_order);
+  hipLaunchKernelGGL(k_psf_order, dim3(1), dim3(256), 0, st, const_cast<JobDesc*>(jobs), n_jobs, pd.G, pd.psf_order,
+                     actions, pd.N, pd.P, err);
   if (tm) tm->begin(3, st);
   hipLaunchKernelGGL(k_psf_eval, dim3(kPsfBlocks, n_jobs), dim3(256), 0, st, jobs, pd.psf_order, mask, field, inten,
                      target, pd.hpsf, pd.N, pd.P, pd.G, pd.vb, pd.psf_partial);
