@@ -257,7 +257,9 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
   float4* U = reinterpret_cast<float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
   float4* I = reinterpret_cast<float4*>(inten + ((size_t)jb.env * G + g) * hw);
   const float2* h = hpsf + (size_t)g * hw;
-#ifdef HBX_PSF_COMMIT_PX1   // A/B switch: one pixel per lane, as k_psf_eval (coalesced shifted-h reads)
+#ifndef HBX_PSF_COMMIT_QUAD   // one pixel per lane, as k_psf_eval (coalesced shifted-h reads): 0.292 -> 0.287 ms
+                             // per 128-job step against four pixels per lane (`make exp EXP=PSF_COMMIT_QUAD`,
+                             // profiles/r02/psf_commit_px1_ab.txt)
   float2* U2 = reinterpret_cast<float2*>(U);
   float* I1 = reinterpret_cast<float*>(I);
 #pragma unroll 4
