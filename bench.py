@@ -46,6 +46,8 @@ def parse():
                     help="env-steps of the numpy oracle timed for cpu_baseline (0 = skip)")
     ap.add_argument("--no-psnr-check", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-pg", action="store_true",
+                    help="world 1: no process group (by default one is built and the RCCL metric gather runs)")
     ap.add_argument("--no-psf", action="store_true", help="skip the incremental-mode measurement")
     ap.add_argument("--psf-steps", type=int, default=200)
     ap.add_argument("--chunk", type=int, default=0,
@@ -56,6 +58,8 @@ def parse():
     ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")
     ap.add_argument("--no-probe", action="store_true", help="skip the all-flip probe-sweep measurement")
     ap.add_argument("--no-ppo", action="store_true", help="skip the 256x256x8 mono (train-PPO) measurement")
+    ap.add_argument("--no-obs", action="store_true",
+                    help="skip the SB3-facing step with all five observations (vecenv_step_obs)")
     ap.add_argument("--no-precision", action="store_true",
                     help="skip the fp32-vs-bf16 intermediate-storage deviation (SURVEY 8d cfg 5)")
     ap.add_argument("--gather-every", type=int, default=1,
@@ -68,16 +72,11 @@ def algorithmic_bytes(N: int, P: int):
     k_rowfwd: read P*N^2/8 mask bits, write P*N^2/2 complex64 (half spectrum)
     k_col:    read P*N^2/2 complex64, write P*N^2 complex64
     k_rowinv: read P*N^2 complex64 + N^2 f32 target
-    k_bits_t:  (bits -> column pipeline, N = 1024) read P*N^2/8 mask bits, write P*N^2/4
-               nibble codes of the transposed bits
-    k_colbits: read the P*N^2/4 codes, write P*N^2 complex64 (no row-spectrum intermediate)
     k_psf_eval:   read the touched plane's field (8 N^2) + group intensity (4 N^2) + target (4 N^2)
     k_psf_commit: accepted envs only: read + write field and intensity (24 N^2)."""
     return {"k_rowfwd": P * N * N // 8 + P * N * N * 4,
             "k_col": P * N * N * 4 + P * N * N * 8,
             "k_rowinv": P * N * N * 8 + N * N * 4,
-            "k_bits_t": P * N * N // 8 + P * N * N // 4,
-            "k_colbits": P * N * N // 4 + P * N * N * 8,
             "k_psf_eval": 16 * N * N,
             "k_psf_commit": 24 * N * N}
 
@@ -332,6 +331,65 @@ def cpu_baseline(n_steps: int, N: int):
                       f"numpy.fft complex128 oracle (oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
 
 
+def cpu_baseline_mono(n_steps: int, N: int = 256):
+    """configs[0] / the PPO shard: env.py's 256x256x8 mono env-step on the float64 numpy
+    oracle (one 8-plane group propagate + PSNR + reward), 1 core."""
+    import numpy as np
+    from oracle import hbx_oracle as O
+    cfg = O.mono_config(N)
+    pre, tgt = O.synthetic_inputs(cfg, 0)
+    env = O.OracleEnv(cfg)
+    env.reset(pre, tgt)
+    acts = np.random.default_rng(2).integers(0, cfg.channels * N * N, n_steps + 2)
+    env.step(int(acts[0]))
+    env.step(int(acts[1]))
+    t0 = time.perf_counter()
+    for a in acts[2:]:
+        env.step(int(a))
+    dt = time.perf_counter() - t0
+    return {"value": n_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_steps} env-steps of the {N}x{N}x8 mono env (env.py), numpy.fft complex128 oracle "
+                      f"(oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
+
+
+def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed):
+    """The step an SB3 learner calls (train-PPO.py:296-322): HologramVecEnv.step with all
+    five observation keys (env.py:176-181) as device tensors, rewards / dones to the host,
+    every step.  The observations are views of buffers the step kernels keep current
+    (ABI v8), so the difference to the bare device step is the recon reconcile copy, the
+    per-step host sync and the Python VecEnv bookkeeping."""
+    import torch
+    from hbx.env import OBS_KEYS, HologramVecEnv
+    vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format="torch",
+                         auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0)
+    vec.reset()
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    n_pix = mcfg.channels * mcfg.height * mcfg.width
+    actions = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda", dtype=torch.int64)
+    for k in range(warmup):
+        vec.step(actions[k])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(warmup, warmup + steps):
+        obs, rew, dones, infos = vec.step(actions[k])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    shapes = {k: list(v.shape) for k, v in obs.items()}
+    views = all(v.data_ptr() == getattr(vec.state, a).data_ptr() for k, v, a in
+                ((k, obs[k], {"state_record": "record", "state": "state_bytes", "pre_model": "pre_model",
+                              "recon_image": "recon", "target_image": "target"}[k]) for k in obs))
+    vec.close()
+    ms = dt / steps * 1e3
+    return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps,
+            "ms_per_step": round(ms, 4), "bare_step_ms": round(bare_ms, 4),
+            "obs_overhead_frac": round(ms / bare_ms - 1.0, 4), "obs_keys": list(obs.keys()),
+            "obs_shapes": shapes, "obs_are_views": views,
+            "note": "HologramVecEnv.step (SB3 VecEnv surface, obs_format='torch', auto_reset on): all five "
+                    "observation keys returned as views of device buffers the step kernels keep current "
+                    "(state as int8, stepped pre-rollback recon_image), rewards / dones copied to the host "
+                    "each step; bare_step_ms is the same workload's step_device without observations"}
+
+
 def psnr_check(vec, N):
     """PSNR delta vs the numpy oracle for env 0's initial state (full 24-plane propagate)."""
     import numpy as np
@@ -390,7 +448,9 @@ def main():
     # HBX_BENCH_REHEARSE_ONE_GPU=1: every rank on cuda:0 over gloo -- rehearses the world > 1
     # code path on a one-GPU box (RCCL refuses two ranks on one device); never a measurement
     rehearse = os.environ.get("HBX_BENCH_REHEARSE_ONE_GPU") == "1"
-    rank, world, local = hd.init(backend="gloo" if rehearse else None)
+    # a process group at every world size (RCCL at N = 1 too): the N = 1 line runs the same
+    # per-step metric gather, barrier and max-over-ranks collectives as the 8-GPU one
+    rank, world, local = hd.init(backend="gloo" if rehearse else None, force=not args.no_pg)
     if rehearse:
         local = 0
     if world != args.gpus and rank == 0:
@@ -400,7 +460,7 @@ def main():
     N, B = args.size, args.envs
     cfg = rgb_config(N)
     CH, G, P = cfg.channels, cfg.groups, cfg.planes
-    gather = (world > 1) and not args.no_gather
+    gather = hd.active() and not args.no_gather
 
     # synthetic, seeded per global env index
     def target_source(i):
@@ -478,8 +538,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
-        step_bytes = sum(abytes[k] for k in timing if k in ("k_rowfwd", "k_col", "k_rowinv", "k_bits_t",
-                                                             "k_colbits")) * B
+        step_bytes = sum(abytes[k] for k in timing if k in ("k_rowfwd", "k_col", "k_rowinv")) * B
         canon = canonical_step_bytes(N, P)
         out = {
             "metric": "env-steps/sec (1024x1024, 24-plane)" if N == 1024 else
@@ -502,19 +561,21 @@ def main():
                        "parallelism": f"env-sharded x{world}" + (
                            f" + metric gather to rank 0 every {args.gather_every} step(s)" if gather else ""),
                        "obs_keys": [],
-                       "obs_note": "the timed step returns reward / psnr / accepted / terminated / truncated "
-                                   "on the device; no observation is assembled (HologramVecEnv(obs_keys=())): "
-                                   "the recon_image write would add 4 N^2 B per env-step (~1.5 % of the "
-                                   "step's 273.7 MB canonical traffic)"},
+                       "obs_note": "the headline times the device step (reward / psnr / accepted / terminated / "
+                                   "truncated stay on the device, HologramVecEnv(obs_keys=())); the SB3-facing "
+                                   "step with all five observations is `vecenv_step_obs`"},
             "ranks_seen": ranks_seen,
             "roofline": roofline,
             "passes": rounded(passes),
             "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-            "step_canonical": {"bytes_per_env_step": canon,
-                               "GBs": round(canon * value / world / 1e9, 1),
-                               "frac": round(canon * value / world / 1e9 / HBM_PEAK_GBS, 4),
-                               "note": "SURVEY 8d canonical traffic (two complex64 round trips per "
-                                       "plane + target + mask) x env-steps/s per GPU, vs 8 TB/s"},
+            "step_alg_frac": round(step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "step_canonical_equivalent": {
+                "bytes_per_env_step": canon,
+                "GBs_equivalent": round(canon * value / world / 1e9, 1),
+                "note": "NOT bandwidth: SURVEY 8d's canonical bytes per env-step (two complex64 round trips "
+                        "per plane + target + mask) x env-steps/s per GPU.  The kernels move fewer bytes "
+                        "(half-spectrum intermediates): their achieved step bandwidth is step_alg_GBs / "
+                        "step_alg_frac"},
             "accept_rate": round(acc_rate, 4),
         }
         if world == 1 and not args.no_psnr_check:
@@ -524,6 +585,12 @@ def main():
     vec.close()
     del vec
     torch.cuda.empty_cache()
+
+    if rank == 0 and world == 1 and not args.no_obs:
+        out["vecenv_step_obs"] = vecenv_step_obs(
+            cfg, B, args.steps, args.warmup, lambda i: target_source(i), lambda i: pre_model_source(i),
+            ms_per_step, 11)
+        torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and args.dbs_flips > 0:
         out["dbs_greedy"] = dbs_prefix(cfg, dbs_mask, dbs_target, args.dbs_flips)
@@ -561,13 +628,27 @@ def main():
         mono = mono_config(256)
         vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup, mcfg=mono)
         ps = pass_table(timing, algorithmic_bytes(256, mono.planes))
-        out["ppo_mono_256"] = {
-            "value": round(B * args.steps / dt, 2), "unit": "env-steps/s", "envs": B,
-            "ms_per_step": round(dt / args.steps * 1e3, 4), "accept_rate": round(acc_rate, 4),
-            "passes": rounded(ps),
-            "note": "env.py / train-PPO.py configuration (256x256, 1 colour group x 8 planes at 515 nm), "
-                    "FFT mode, same env semantics as the headline"}
         vec.close()
+        if rank == 0:
+            dom = max(ps, key=lambda n: ps[n]["avg_ms"])
+            mono_ms = dt / args.steps * 1e3
+            out["ppo_mono_256"] = {
+                "value": round(B * args.steps / dt, 2), "unit": "env-steps/s", "envs": B,
+                "ms_per_step": round(mono_ms, 4), "accept_rate": round(acc_rate, 4),
+                "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ps[dom]["achieved_GBs"], 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ps[dom]["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                             "kernel_avg_ms": round(ps[dom]["avg_ms"], 4)},
+                "passes": rounded(ps),
+                "note": "configs[0] / train-PPO.py's env (env.py, 256x256, 1 colour group x 8 planes at 515 nm), "
+                        "128 envs per GPU, FFT mode, same env semantics as the headline"}
+            if not args.no_obs:
+                out["ppo_mono_256"]["vecenv_step_obs"] = vecenv_step_obs(
+                    mono, B, args.steps, args.warmup,
+                    lambda i: target_source(i)[:1, :256, :256].contiguous(),
+                    lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12)
+            if args.cpu_sample > 0:
+                out["ppo_mono_256"]["cpu_baseline"] = cpu_baseline_mono(max(40, 25 * args.cpu_sample))
 
     if rank == 0:
         if world == 1 and args.cpu_sample > 0:
@@ -579,6 +660,7 @@ def main():
                 except Exception as e:  # scipy is optional on the box
                     out["cpu_baseline_scipy"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
+    hd.shutdown()
 
 
 if __name__ == "__main__":

@@ -142,55 +142,12 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       const double a = -2.0 * M_PI * (double)((t * k1) % N) / (double)N;
       tw[(size_t)k1 * R + t] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
-  if (R == 0) {   // N = 896: fused three-pass path unless HBX_GENERIC896=1 (the composed path)
-    const char* ev = std::getenv("HBX_GENERIC896");
-    pd.fused896 = (ev && ev[0] && ev[0] != '0') ? 0 : 1;
-  }
   if (R == 0)   // N = 896: [k1 < 28][t < 32] = W896^{t k1}
     for (int k1 = 0; k1 < 28; ++k1)
       for (int t = 0; t < 32; ++t) {
         const double a = -2.0 * M_PI * (double)(t * k1) / (double)N;
         tw[(size_t)k1 * 32 + t] = make_float2((float)std::cos(a), (float)std::sin(a));
       }
-  if (N == 1024) {  // whole-wave FFT tables of the column pass: tw1[k1][L], tw2[m1][l0]
-    for (int k1 = 0; k1 < 16; ++k1)
-      for (int L = 0; L < 64; ++L) {
-        const double a = -2.0 * M_PI * (double)(L * k1) / 1024.0;
-        tw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
-      }
-    for (int m1 = 0; m1 < 16; ++m1)
-      for (int l0 = 0; l0 < 4; ++l0) {
-        const double a = -2.0 * M_PI * (double)(l0 * m1) / 64.0;
-        tw.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
-      }
-  }
-  if (N == 1024) {  // class tables of the bits -> column pass (hbx_internal.hpp kTwClassOff)
-    tw.resize((size_t)hbx::kTwClassOff + 33 * (size_t)hbx::kTwClassStride, make_float2(0.f, 0.f));
-    for (int c = 0; c <= 32; ++c) {
-      float2* ct = tw.data() + hbx::kTwClassOff + (size_t)c * hbx::kTwClassStride;
-      const int k1 = c % 32;
-      for (int k = 0; k < 8; ++k)
-        for (int v = 0; v < 16; ++v) {
-          double re = 0.0, im = 0.0;
-          for (int jb = 0; jb < 4; ++jb)
-            if ((v >> jb) & 1) {
-              const double a = -2.0 * M_PI * (double)((k1 * (4 * k + jb)) % 32) / 32.0;
-              re += std::cos(a);
-              im += std::sin(a);
-            }
-          ct[k * 16 + v] = make_float2((float)re, (float)im);
-        }
-      for (int n2 = 0; n2 < 16; ++n2) {
-        const double a = -2.0 * M_PI * (double)((c * n2) % 1024) / 1024.0;
-        ct[128 + n2] = make_float2((float)std::cos(a), (float)std::sin(a));
-      }
-      const double a = -2.0 * M_PI * (double)(c % 64) / 64.0;
-      ct[144] = make_float2((float)std::cos(a), (float)std::sin(a));
-    }
-    // opt-in A/B switch: measured slower than the three-pass path (colbits)
-    const char* ev = std::getenv("HBX_COLBITS");
-    pd.colbits = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
-  }
   {
     const char* ev = std::getenv("HBX_WALK_SPLIT");   // A/B switch: the v5 three-launch walk batches
     p->walk_split = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
@@ -279,8 +236,8 @@ int hbx_plan_set_precision(hbx_plan_t p, int32_t precision) {
   if (rc) return rc;
   if (precision < HBX_PRECISION_F32 || precision > HBX_PRECISION_F16_STORE)
     return fail(HBX_ERR_INVALID, "precision must be HBX_PRECISION_F32, _BF16_STORE or _F16_STORE");
-  if (precision != HBX_PRECISION_F32 && (p->pd.R == 0 || p->pd.colbits))
-    return fail(HBX_ERR_UNSUPPORTED, "reduced-precision intermediates: N = 64 / 256 / 1024 three-pass path only");
+  if (precision != HBX_PRECISION_F32 && p->pd.R == 0)
+    return fail(HBX_ERR_UNSUPPORTED, "reduced-precision intermediates: N = 64 / 256 / 1024 only");
   p->pd.store_kind = precision;
   return HBX_OK;
 }
@@ -294,8 +251,7 @@ int hbx_plan_precision(hbx_plan_t p) {
 int hbx_plan_pipeline(hbx_plan_t p) {
   int rc = check_plan(p);
   if (rc) return rc;
-  if (p->pd.R == 0) return p->pd.fused896 ? HBX_PIPE_THREE_PASS : HBX_PIPE_GENERIC;
-  return (p->pd.R == 32 && p->pd.colbits) ? HBX_PIPE_COLBITS : HBX_PIPE_THREE_PASS;
+  return HBX_PIPE_THREE_PASS;   // the only pipeline built since ABI v8
 }
 
 }  // extern "C"
@@ -375,6 +331,8 @@ EnvDev env_dev(const hbx_env_buffers_t* e) {
   d.steps = e->steps; d.flip_count = e->flip_count; d.sustained = e->sustained;
   d.imp_changes = e->imp_changes; d.imp_values = e->imp_values; d.t_psnr_diff = e->t_psnr_diff;
   d.imp_count = e->imp_count;
+  d.state_bytes = e->state_bytes;
+  d.recon_pending = e->recon_pending;
   return d;
 }
 
@@ -394,7 +352,16 @@ EnvDev env_offset(const EnvDev& d, size_t e0, int CH, int G, int N) {
   o.imp_changes = d.imp_changes ? d.imp_changes + e0 * (size_t)d.imp_count : nullptr;
   o.imp_values = d.imp_values ? d.imp_values + e0 * (size_t)d.imp_count : nullptr;
   o.t_psnr_diff = d.t_psnr_diff ? d.t_psnr_diff + e0 : nullptr;
+  o.state_bytes = d.state_bytes ? d.state_bytes + e0 * (size_t)CH * N * N : nullptr;
+  o.recon_pending = d.recon_pending ? d.recon_pending + e0 : nullptr;
   return o;
+}
+
+// the observation buffers a step writes need the caches they mirror
+int check_obs_buffers(const hbx_env_buffers_t* e) {
+  if (e->recon && (!e->intensity || !e->recon_pending))
+    return fail(HBX_ERR_INVALID, "env.recon needs env.intensity and env.recon_pending");
+  return HBX_OK;
 }
 
 // full propagation of n_ids envs (absolute ids from env_ids, or 0..n_ids-1)
@@ -494,9 +461,36 @@ int hbx_env_reset(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const
     rc = ensure_hpsf(p, st);
     if (rc) return rc;
   }
+  rc = check_obs_buffers(e);
+  if (rc) return rc;
   EnvDev ed = env_dev(e);
-  return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed,
-                        reinterpret_cast<float2*>(e->field), st);
+  rc = propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed,
+                      reinterpret_cast<float2*>(e->field), st);
+  if (rc) return rc;
+  HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, e->state_bytes, e->intensity, e->recon, e->recon_pending,
+                               CH, pd.G, (size_t)pd.N * pd.N, st));
+  return HBX_OK;
+}
+
+int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const int32_t* env_ids,
+                     int32_t n_ids, int32_t what, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!e) return fail(HBX_ERR_INVALID, "null env buffers");
+  if (what & ~(HBX_OBS_STATE | HBX_OBS_RECON)) return fail(HBX_ERR_INVALID, "what: HBX_OBS_STATE | HBX_OBS_RECON");
+  const bool st_on = (what & HBX_OBS_STATE) != 0, rc_on = (what & HBX_OBS_RECON) != 0;
+  if (st_on && (!e->mask || !e->state_bytes)) return fail(HBX_ERR_INVALID, "HBX_OBS_STATE needs mask and state_bytes");
+  if (rc_on && (!e->recon || !e->intensity || !e->recon_pending))
+    return fail(HBX_ERR_INVALID, "HBX_OBS_RECON needs recon, intensity and recon_pending");
+  if (n_env < 0) return fail(HBX_ERR_INVALID, "n_env");
+  const int n = env_ids ? n_ids : n_env;
+  if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_ids");
+  HBX_HIP(hipSetDevice(p->device));
+  const PlanDev& pd = p->pd;
+  HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, st_on ? e->state_bytes : nullptr, e->intensity,
+                               rc_on ? e->recon : nullptr, e->recon_pending, pd.G * pd.P, pd.G,
+                               (size_t)pd.N * pd.N, (hipStream_t)stream));
+  return HBX_OK;
 }
 
 int hbx_field_refresh(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const int32_t* env_ids,
@@ -525,6 +519,7 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
       !e->intensity || !e->field)
     return fail(HBX_ERR_INVALID, "env buffers incomplete (incremental mode needs field + intensity)");
   if (!p->pd.hpsf) return fail(HBX_ERR_INVALID, "incremental mode: call hbx_env_reset with env.field first");
+  if (e->recon) return fail(HBX_ERR_INVALID, "env.recon (the pre-rollback recon_image) needs the FFT-mode step");
   if (prm->accept_rule != HBX_ACCEPT_ENV && prm->accept_rule != HBX_ACCEPT_DBS)
     return fail(HBX_ERR_INVALID, "accept_rule");
   if (prm->reward_kind != HBX_REWARD_PSNR && prm->reward_kind != HBX_REWARD_IMPORTANCE)
@@ -584,11 +579,18 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   const PlanDev& pd = p->pd;
   const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
   const size_t hw = (size_t)N * N;
-  const bool want_inten = group_intensity || e->intensity;
+  rc = check_obs_buffers(e);
+  if (rc) return rc;
+  if (e->recon && group_intensity)
+    return fail(HBX_ERR_INVALID, "give group_intensity or env.recon, not both (recon holds the stepped group)");
+  const bool to_recon = e->recon != nullptr;
+  const bool want_inten = !to_recon && (group_intensity || e->intensity);
   if (want_inten) {
     rc = ensure_job_inten(p);
     if (rc) return rc;
   }
+  PlanDev pdx = p->pd;            // with recon, k_rowinv writes the stepped group straight into it
+  pdx.inten_by_env = to_recon ? 1 : 0;
   EnvParams ep;
   ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
@@ -598,9 +600,12 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
     const EnvDev ed = env_offset(base, b0, CH, G, N);
+    float* rec = to_recon ? e->recon + (size_t)b0 * G * hw : nullptr;
+    if (to_recon)   // the previous step's group: recon and intensity agree again before it is overwritten
+      HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
-    HBX_HIP(hbx::run_jobs(pd, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,
-                          want_inten ? p->job_inten : nullptr, nullptr, st));
+    HBX_HIP(hbx::run_jobs(pdx, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,
+                          to_recon ? rec : (want_inten ? p->job_inten : nullptr), nullptr, st));
     HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),
                                           p->optics.rel_scale, p->optics.peak,
                                           reward ? reward + b0 : nullptr, psnr ? psnr + b0 : nullptr,
@@ -611,7 +616,7 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     if (group_intensity)
       HBX_HIP(hipMemcpyAsync(group_intensity + (size_t)b0 * hw, p->job_inten, (size_t)n * hw * sizeof(float),
                              hipMemcpyDeviceToDevice, st));
-    if (e->intensity)
+    if (e->intensity && !to_recon)
       HBX_HIP(hbx::launch_scatter_intensity(p->jobs, n, p->job_inten, e->intensity + (size_t)b0 * G * hw, G,
                                             hw, p->accept_flag, st));
   }

@@ -298,9 +298,6 @@ __device__ __forceinline__ void fft_group(T (&v)[R], int t, const Scratch& sc, c
   // keep the twiddle loads local to each FFT: without this barrier the
   // compiler CSEs / hoists them across calls and pins 2R VGPRs for good
   asm volatile("" ::: "memory");
-#ifdef HBX_NO_FFT  // access-pattern ceiling experiments only (tools/): data moves, no arithmetic
-  return;
-#endif
   if constexpr (SCALAR) {
     static_assert(std::is_same<T, float2>::value, "scalar FFT works on float2");
     dft_reg_scalar<R, INV>(v);
@@ -336,9 +333,6 @@ __device__ __forceinline__ void fft_group(T (&v)[R], int t, const Scratch& sc, c
 template <int R, bool INV, bool SCALAR = false, class T>
 __device__ __forceinline__ void fft_group_split(T (&v)[R], int t, float* sc, const float2* tw) {
   asm volatile("" ::: "memory");
-#ifdef HBX_NO_FFT
-  return;
-#endif
   if constexpr (SCALAR) {
     static_assert(std::is_same<T, float2>::value, "scalar FFT works on float2");
     dft_reg_scalar<R, INV>(v);
@@ -403,125 +397,6 @@ __device__ __forceinline__ float2 mirror_conj(const T (&v)[R], int k2, int t, in
   const float2 own = make_float2(v[(R - k2) & (R - 1)].x, v[(R - k2) & (R - 1)].y);
   const float2 z = (t == 0) ? own : p;
   return conjf2(z);
-}
-
-// ---------------------------------------------------------------------------
-// Whole-wave 1024-point FFT: 64 lanes x 16 registers (half the registers per
-// line of the 32-lane group FFT above, so the column pass can keep the next
-// line, this line's transfer function and the line itself in flight at three
-// waves per SIMD).  Three-step decomposition, n = L + 64 j, k = k1 + 16 m:
-//   A[L][k1]  = sum_j x[L + 64 j] W16^{j k1}            16-point DFT, registers
-//   A'        = A W1024^{L k1}                           LDS table tw1[k1][L]
-//   transpose: lane L' = l0 + 4 q takes A'[l0 + 4 l1][q], l1 = 0..15 (LDS)
-//   C[l0][m1] = sum_l1 A'[l0 + 4 l1][q] W16^{l1 m1}      16-point DFT, registers
-//   C'        = C W64^{l0 m1}                            LDS table tw2[m1][l0]
-//   X[q + 16 m1 + 256 m2] = sum_l0 C'[l0][m1] W4^{l0 m2} 4-point DFT across the
-//                                                        lanes of a quad (DPP)
-// The spectrum is left in "slot order": lane L' = l0 + 4 q, register m1 holds
-//   X[ky], ky = q + 16 m1 + 256 bitrev2(l0)          (wave_ky_base + 16 m1).
-// The inverse takes slot order in and returns natural order (lane L, register
-// j holds x[L + 64 j]): it is the adjoint of the forward network.
-// ---------------------------------------------------------------------------
-constexpr int kWaveScratch = 16 * 68;   // float2 per wave: [16][64 + 4] transpose tile
-
-__device__ __forceinline__ int wave_ky_base(int L) {
-  const int l0 = L & 3;
-  return (L >> 2) + 256 * (((l0 & 1) << 1) | (l0 >> 1));
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-// value held by lane L ^ 1 / L ^ 2 (quad_perm [1,0,3,2] / [2,3,0,1])
-__device__ __forceinline__ float2 quad_xor1(float2 a) { return make_float2(dpp_mov<0xB1>(a.x), dpp_mov<0xB1>(a.y)); }
-__device__ __forceinline__ float2 quad_xor2(float2 a) { return make_float2(dpp_mov<0x4E>(a.x), dpp_mov<0x4E>(a.y)); }
-
-// forward 4-point DFT over the quad (DIF): lane l0 ends with Y[bitrev2(l0)]
-__device__ __forceinline__ void quad_dft4_fwd(float2 (&v)[16], int l0) {
-  const float s_hi = (l0 & 2) ? -1.0f : 1.0f;
-  const float s_odd = (l0 & 1) ? -1.0f : 1.0f;
-  const bool rot = (l0 & 3) == 3;   // (y_lo - y_hi) * (-i) on lane 3
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float2 p = quad_xor2(v[r]);
-    float2 d = make_float2(fmaf(s_hi, v[r].x, p.x), fmaf(s_hi, v[r].y, p.y));
-    v[r] = rot ? make_float2(d.y, -d.x) : d;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float2 q = quad_xor1(v[r]);
-    v[r] = make_float2(fmaf(s_odd, v[r].x, q.x), fmaf(s_odd, v[r].y, q.y));
-  }
-}
-
-// adjoint of quad_dft4_fwd (inverse sign, DIT): lane l0 holds Y[bitrev2(l0)] in,
-// y[l0] = sum_m Y[m] i^{m l0} out
-__device__ __forceinline__ void quad_dft4_inv(float2 (&v)[16], int l0) {
-  const bool hi = (l0 & 2) != 0;
-  const float s_hi = hi ? -1.0f : 1.0f;
-  const float s_odd = (l0 & 1) ? -1.0f : 1.0f;
-  const bool odd = (l0 & 1) != 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float2 q = quad_xor1(v[r]);
-    v[r] = make_float2(fmaf(s_odd, v[r].x, q.x), fmaf(s_odd, v[r].y, q.y));
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float2 p = quad_xor2(v[r]);
-    const float2 lo = hi ? p : v[r];
-    const float2 u = hi ? v[r] : p;
-    const float2 cu = odd ? make_float2(-u.y, u.x) : u;   // * (+i) on odd quads lanes
-    v[r] = make_float2(fmaf(s_hi, cu.x, lo.x), fmaf(s_hi, cu.y, lo.y));
-  }
-}
-
-// natural order in (v[j] = x[L + 64 j]) -> slot order out
-__device__ __forceinline__ void wave_fft1024_fwd(float2 (&v)[16], int L, float2* scr,
-                                                 const float2* tw1, const float2* tw2) {
-  asm volatile("" ::: "memory");
-  // pin the first use of the input here: otherwise the scheduler hoists the
-  // register-only first radix stages above the previous line's stores, which
-  // waits for this line's loads far too early
-#pragma unroll
-  for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(v[j].x), "+v"(v[j].y));
-  const int l0 = L & 3, q = L >> 2;
-  dft_reg<16, false>(v);
-#pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw1[k1 * 64 + L]);
-  wave_sync();
-#pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) scr[k1 * 68 + L] = v[k1];
-  wave_sync();
-#pragma unroll
-  for (int l1 = 0; l1 < 16; ++l1) v[l1] = scr[q * 68 + l0 + 4 * l1];
-  wave_sync();
-  dft_reg<16, false>(v);
-#pragma unroll
-  for (int m1 = 1; m1 < 16; ++m1) v[m1] = cmul(v[m1], tw2[m1 * 4 + l0]);
-  quad_dft4_fwd(v, l0);
-}
-
-// slot order in -> natural order out (unnormalised inverse DFT)
-__device__ __forceinline__ void wave_fft1024_inv(float2 (&v)[16], int L, float2* scr,
-                                                 const float2* tw1, const float2* tw2) {
-  asm volatile("" ::: "memory");
-  const int l0 = L & 3, q = L >> 2;
-  quad_dft4_inv(v, l0);
-#pragma unroll
-  for (int m1 = 1; m1 < 16; ++m1) v[m1] = cmulc(v[m1], tw2[m1 * 4 + l0]);
-  dft_reg<16, true>(v);
-  wave_sync();
-#pragma unroll
-  for (int l1 = 0; l1 < 16; ++l1) scr[q * 68 + l0 + 4 * l1] = v[l1];
-  wave_sync();
-#pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) v[k1] = scr[k1 * 68 + L];
-  wave_sync();
-#pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmulc(v[k1], tw1[k1 * 64 + L]);
-  dft_reg<16, true>(v);
 }
 
 // ---------------------------------------------------------------------------

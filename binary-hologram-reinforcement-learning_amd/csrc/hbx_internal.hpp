@@ -41,37 +41,24 @@ struct JobDesc {
 };
 
 // Intermediate layout of the fused N = R^2 path (hbx_passes.hip).  The row
-// passes run blocks of row_nt(R) threads = panel_rows(R) rows; a plane of L
-// lines is stored as N / PAN panels [L][PAN] (PAN = panel_rows), panel q at
-// q * panel_stride.  The pad keeps consecutive panels off the same memory
-// channel: a column-pass line touches one 64-B piece of every panel, and with
-// power-of-two panel strides those pieces all land on one channel.
-#ifndef HBX_ROW_NT
-#define HBX_ROW_NT 256
-#endif
-#ifndef HBX_PANEL_PAD
-#define HBX_PANEL_PAD 0
-#endif
-#ifndef HBX_PANEL_A   // rows per panel of A (0: one panel of N rows = column-major lines; values
-                      // below the row pass's block height round up to it).  Panels of the
-                      // block height make every k_rowfwd store contiguous (tools/membw2.hip:
-                      // 0.69 ms for the 128-job A vs 1.19 ms as 64-B pieces of line-major A)
-                      // and cost k_col2's line reads nothing (2.54 vs 2.55 ms replayed)
-#define HBX_PANEL_A 8
-#endif
-#ifndef HBX_PANEL_B   // rows per panel of B
-#define HBX_PANEL_B 16
-#endif
-__host__ __device__ constexpr int row_nt(int R) { return R == 32 ? HBX_ROW_NT : 256; }
+// passes run blocks of row_nt(R) = 256 threads = panel_rows(R) rows; a plane of
+// L lines is stored as N / PAN panels [L][PAN], panel q at q * PAN * L.  A is
+// kept in panels of the row block height (8 rows at N = 1024: every k_rowfwd
+// store is contiguous -- 0.69 ms for the 128-job A vs 1.19 ms as 64-B pieces of
+// line-major A, tools/membw2.hip -- and k_col2's line reads cost nothing), B in
+// panels of 16 rows (k_col2 writes 128-B pieces; 8-row B panels made its
+// stores cost 1 ms more, 32 / 64 rows or a pad between panels were slower too:
+// DESIGN.md 4).
+constexpr int kPanelA = 8;
+constexpr int kPanelB = 16;
+__host__ __device__ constexpr int row_nt(int R) { return 256; }
 __host__ __device__ constexpr int panel_rows(int R) { return row_nt(R) / R; }
 __host__ __device__ constexpr int pan_of(int R, int rows) {
   return rows <= 0 || rows >= R * R ? R * R : (rows < panel_rows(R) ? panel_rows(R) : rows);
 }
-__host__ __device__ constexpr int pan_a(int R) { return pan_of(R, HBX_PANEL_A); }
-__host__ __device__ constexpr int pan_b(int R) { return pan_of(R, HBX_PANEL_B); }
-__host__ __device__ constexpr int panel_stride(int R, int L, int PAN) {
-  return L * PAN + (PAN < R * R ? HBX_PANEL_PAD : 0);
-}
+__host__ __device__ constexpr int pan_a(int R) { return pan_of(R, kPanelA); }
+__host__ __device__ constexpr int pan_b(int R) { return pan_of(R, kPanelB); }
+__host__ __device__ constexpr int panel_stride(int R, int L, int PAN) { return L * PAN; }
 // float2 elements per intermediate plane: A (half spectrum, N/2 lines), B (N lines)
 __host__ __device__ constexpr size_t plane_a_elems(int R) {
   return (size_t)(R * R / pan_a(R)) * panel_stride(R, R * R / 2, pan_a(R));
@@ -135,24 +122,14 @@ struct PlanDev {
   double* psf_partial; // [max_jobs][kPsfBlocks][2]
   int32_t* psf_order;  // [max_jobs] jobs sorted by colour group (launch order)
   float* zero_row;     // [N] zeros: the target row of a propagation without a target
-  int colbits;         // N = 1024: bits -> column pass without the A intermediate (hbx_colbits.hip)
   int store_kind;      // HBX_PRECISION_*: rounding of the pass intermediates (0 = f32, the product)
-  int fused896;        // N = 896: fused three-pass path (hbx_passes896.hip); 0 = composed (hbx_generic.hip)
+  int inten_by_env;    // intensity output rows: 0 = job-major [job][N][N]; 1 = env-major
+                       // [env][G][N][N] at (job.env, job.group) (the obs recon buffer, ABI v8)
   PassTimer* timer;    // nullable
 };
 
-#ifndef HBX_PSF_BLOCKS   // A/B switch: `make exp EXP=PSF_BLOCKS=128`
-#define HBX_PSF_BLOCKS 128   // measured 128 > 256 > 64 > 32 (profiles/r01_psf_blocks_ab.txt)
-#endif
-constexpr int kPsfBlocks = HBX_PSF_BLOCKS;   // blocks per job of the incremental-field kernels
-
-// N = 1024 class tables appended to PlanDev::tw (hbx_colbits.hip): class c = 0..32 at
-// kTwClassOff + c * kTwClassStride: [8][16] nibble tables sum_j v_j W32^{(c mod 32)(4k + j)},
-// [16] W1024^{c n2}, [1] W64^c
-constexpr int kTwClassOff = 1024 + 16 * 64 + 16 * 4;
-constexpr int kTwClassStride = 160;
-hipError_t launch_colbits(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
-                          hipStream_t st);
+constexpr int kPsfBlocks = 128;   // blocks per job of the incremental-field kernels
+                                  // (measured 128 > 256 > 64 > 32, profiles/r01_psf_blocks_ab.txt)
 
 struct EnvDev {
   uint64_t* mask;
@@ -169,6 +146,8 @@ struct EnvDev {
   const double* imp_values;
   const double* t_psnr_diff;  // [B] nullable
   int imp_count;
+  int8_t* state_bytes;        // [B][CH][H][W] obs["state"] mirror of the mask bits (nullable, ABI v8)
+  int32_t* recon_pending;     // [B] group the next step reconciles (nullable; with recon)
 };
 
 struct EnvParams {
@@ -184,13 +163,9 @@ struct EnvParams {
 // field_out (nullable): [env][G*P][N][N] complex field of every propagated plane
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, float2* field_out, hipStream_t st);
-// generic propagation (N = 896, hbx_generic.hip): prep -> 2-D FFT -> H -> inverse
-// 2-D FFT -> |U|^2 mean + partial sums, on the transposing row-FFT kernel
 // fused three-pass propagation at N = 896 (hbx_passes896.hip)
 hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                         const float* target, float* inten_out, float2* field_out, hipStream_t st);
-hipError_t run_jobs_generic(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint64_t* mask,
-                            const float* target, float* inten_out, float2* field_out, hipStream_t st);
 // 2-D FFT of n_planes [N][N] complex planes in a (result in a; b is scratch of
 // the same size).  Unnormalised both ways.
 hipError_t run_fft2d(const PlanDev& pd, float2* a, float2* b, int n_planes, bool inverse,
@@ -282,5 +257,12 @@ hipError_t launch_scatter_intensity(const JobDesc* jobs, int n_jobs, const float
                                     int G, size_t hw, const int32_t* accept_flag, hipStream_t st);
 hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, double count, int rel,
                        double peak, hipStream_t st);
+// observation mirrors (ABI v8): reconcile the previous step's group between recon and
+// intensity (recon_pending), and rebuild state_bytes / recon of listed envs
+hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
+                                  size_t hw, hipStream_t st);
+hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
+                           const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
+                           hipStream_t st);
 
 }  // namespace hbx

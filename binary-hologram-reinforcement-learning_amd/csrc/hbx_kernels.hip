@@ -164,6 +164,7 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     if (term_out) term_out[b] = 0;
     if (trunc_out) trunc_out[b] = 0;
     if (accept_flag) accept_flag[b] = 0;
+    if (env.recon_pending) env.recon_pending[b] = 0;
     return;
   }
   const int g = jb.group;
@@ -197,8 +198,12 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
   if (reject) {                                           // env.py:191-196
     flips -= 1;
   } else {
-    env.mask[((size_t)b * CH + ch) * (size_t)H * (W / 64) + (size_t)(jb.flip_pix / W) * (W / 64) +
-             (jb.flip_pix % W) / 64] ^= (1ull << ((jb.flip_pix % W) & 63));
+    uint64_t* word = env.mask + ((size_t)b * CH + ch) * (size_t)H * (W / 64) + (size_t)(jb.flip_pix / W) * (W / 64) +
+                     (jb.flip_pix % W) / 64;
+    const uint64_t nw = *word ^ (1ull << ((jb.flip_pix % W) & 63));
+    *word = nw;
+    if (env.state_bytes)                                 // obs["state"] mirror (env.py:177 hands out self.state)
+      env.state_bytes[((size_t)b * CH + ch) * (size_t)H * W + jb.flip_pix] = (int8_t)((nw >> ((jb.flip_pix % W) & 63)) & 1ull);
     st[3 * g] = js[0]; st[3 * g + 1] = js[1]; st[3 * g + 2] = js[2];
     env.max_psnr_diff[b] = fmax(env.max_psnr_diff[b], diff);     // env.py:198
     const double sr = (double)flips / (double)steps;              // env.py:200
@@ -223,6 +228,7 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
   if (term_out) term_out[b] = term ? 1 : 0;
   if (trunc_out) trunc_out[b] = trunc ? 1 : 0;
   if (accept_flag) accept_flag[b] = reject ? 0 : 1;
+  if (env.recon_pending) env.recon_pending[b] = reject ? -(g + 1) : (g + 1);
 }
 
 // env_group.py:254-255: reward = importance_ranks[argmin |psnr_change_list -
@@ -366,6 +372,57 @@ __global__ void k_scatter_intensity(const JobDesc* __restrict__ jobs, const floa
     d[k] = s[k];
 }
 
+// obs["recon_image"] (ABI v8): the previous step left its group's stepped intensity in
+// recon[b][g]; before this step overwrites a group, make the two caches agree again --
+// accepted (+g+1): intensity[b][g] <- recon[b][g]; rolled back (-(g+1)): recon[b][g] <-
+// intensity[b][g] (env.py:191-196 restores the state; the obs of the NEXT step shows the
+// restored means of the groups it does not touch).  grid (x, n envs)
+__global__ void k_recon_reconcile(const int32_t* __restrict__ pending, float* __restrict__ recon,
+                                  float* __restrict__ intensity, int G, size_t hw) {
+  const int b = blockIdx.y;
+  const int p = pending[b];
+  if (p == 0) return;
+  const int g = (p > 0 ? p : -p) - 1;
+  const size_t off = ((size_t)b * G + g) * hw;
+  const float4* s = reinterpret_cast<const float4*>((p > 0 ? recon : intensity) + off);
+  float4* d = reinterpret_cast<float4*>((p > 0 ? intensity : recon) + off);
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < hw / 4; k += (size_t)gridDim.x * blockDim.x)
+    d[k] = s[k];
+}
+
+// rebuild the observation mirrors of listed envs: state_bytes from the mask bits (one
+// 64-bit word -> 64 bytes per thread), recon <- intensity, pending <- 0.  grid (x, n_ids)
+__global__ void k_obs_sync(const int32_t* __restrict__ env_ids, const uint64_t* __restrict__ mask,
+                           int8_t* __restrict__ state_bytes, const float* __restrict__ intensity,
+                           float* __restrict__ recon, int32_t* __restrict__ pending, int CH, int G, size_t hw) {
+  const int i = blockIdx.y;
+  const int e = env_ids ? env_ids[i] : i;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (state_bytes) {
+    const size_t words = (size_t)CH * hw / 64;
+    const uint64_t* m = mask + (size_t)e * words;
+    uint4* o = reinterpret_cast<uint4*>(state_bytes + (size_t)e * CH * hw);
+    for (size_t w = t0; w < words; w += stride) {
+      const uint64_t x = m[w];
+      uint32_t q[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {    // bytes 4k .. 4k+3 = bits 4k .. 4k+3
+        const uint32_t n = (uint32_t)(x >> (4 * k)) & 0xfu;
+        q[k] = (n & 1u) | ((n & 2u) << 7) | ((n & 4u) << 14) | ((n & 8u) << 21);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[4 * w + k] = make_uint4(q[4 * k], q[4 * k + 1], q[4 * k + 2], q[4 * k + 3]);
+    }
+  }
+  if (recon) {
+    const float4* s = reinterpret_cast<const float4*>(intensity + (size_t)e * G * hw);
+    float4* d = reinterpret_cast<float4*>(recon + (size_t)e * G * hw);
+    for (size_t k = t0; k < (size_t)G * hw / 4; k += stride) d[k] = s[k];
+    if (t0 == 0 && pending) pending[e] = 0;
+  }
+}
+
 // psnr from chan_stats
 __global__ void k_psnr(const double* __restrict__ chan_stats, int n, int G, double* __restrict__ psnr,
                        double count, int rel_scale, double peak) {
@@ -453,6 +510,20 @@ hipError_t launch_scatter_intensity(const JobDesc* jobs, int n_jobs, const float
                                     int G, size_t hw, const int32_t* accept_flag, hipStream_t st) {
   hipLaunchKernelGGL(k_scatter_intensity, dim3(64, n_jobs), dim3(256), 0, st, jobs, src, cache, G, hw,
                      accept_flag);
+  return hipGetLastError();
+}
+hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
+                                  size_t hw, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_recon_reconcile, dim3(32, n), dim3(256), 0, st, pending, recon, intensity, G, hw);
+  return hipGetLastError();
+}
+hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
+                           const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
+                           hipStream_t st) {
+  if (n_ids <= 0 || (!state_bytes && !recon)) return hipSuccess;
+  hipLaunchKernelGGL(k_obs_sync, dim3(64, n_ids), dim3(256), 0, st, env_ids, mask, state_bytes, intensity, recon,
+                     pending, CH, G, hw);
   return hipGetLastError();
 }
 hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, double count, int rel,

@@ -54,10 +54,10 @@ __device__ __forceinline__ float2 store_round(float2 v) {
   }
 }
 
-// Threads per block of the row passes at N = 1024 (row_nt, hbx_internal.hpp).
-// -DHBX_ROW_NT=512 gives 16 rows per block (conflict-free swizzle above) but
-// only one 143-KB block per CU, whose barriers then stall the whole CU:
-// measured k_rowfwd 1.17 -> 1.54 ms, k_rowinv 2.01 -> 2.62 ms.
+// Threads per block of the row passes (row_nt, hbx_internal.hpp).  512-thread
+// row blocks (16 rows) were measured slower at N = 1024 -- one 143-KB block per
+// CU, whose barriers stall the whole CU: k_rowfwd 1.17 -> 1.54 ms, k_rowinv
+// 2.01 -> 2.62 ms.
 template <int R>
 constexpr int kRowNT = row_nt(R);
 
@@ -79,20 +79,15 @@ using LayoutB = PanelLine<R, R * R, pan_b(R)>;
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
-// Row blocks per k_rowfwd workgroup (HBX_ROWFWD_ITER): a workgroup walks RIT
+// Row blocks per k_rowfwd workgroup (rowfwd_iters): a workgroup walks RIT
 // consecutive row blocks of one plane pair, so the stores of block i stay in
 // flight under the bit loads and row FFTs of block i + 1 (the next rows' mask
 // words are prefetched before the stores are issued: vmcnt counts loads and
 // stores in order, so waiting for them never waits for the stores).  With one
 // row block per workgroup the load -> FFT -> LDS tile -> store chain of the
 // two co-resident workgroups ran nearly serial.
-#ifndef HBX_ROWFWD_ITER
-#define HBX_ROWFWD_ITER 4
-#endif
 template <int R>
-constexpr int rowfwd_iters() {
-  return (R == 32 && (R * R / (kRowNT<R> / R)) % HBX_ROWFWD_ITER == 0) ? HBX_ROWFWD_ITER : 1;
-}
+constexpr int rowfwd_iters() { return R == 32 ? 4 : 1; }
 
 template <int R, int NT, int SK>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
@@ -334,60 +329,24 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 // Pass 2
 // ---------------------------------------------------------------------------
 // Column pass, one lane group per input line and both of its output lines:
-// forward FFT over y -> Z; Z H and Z conj H from the same H(kx, .) row (H is
-// even in fx and fy); inverse FFT of Z H -> B line kx, conjugate of the
-// inverse FFT of Z conj H -> B line N - kx (kx = 0: (Z + M)/2 -> line 0 and
-// -i (Z - M)/2 with the H(N/2) row -> line N/2, M = conj Z(-ky)).  One
-// forward FFT per input line instead of one per output line (the two-role
-// k_col), one A read, one H read, and no cross-group traffic: every LDS
-// hand-off stays inside the group's own scratch (wave_sync only).  The next
-// line's loads go into v as soon as line kx is stored and fly under the
-// second inverse FFT.  Scalar-f32 FFTs here: with two lines in registers the
-// packed variant (hbx_fft.hpp) spills.
-#ifndef HBX_COL2_SCALAR
-#ifdef HBX_COL2_PACKED   // A/B switch: `make exp EXP=COL2_PACKED`
-#define HBX_COL2_SCALAR false
-#else
-#define HBX_COL2_SCALAR true
-#endif
-#endif
-#if HBX_COL2_SCALAR
-#define COL2_T float2
-#define COL2_LD(x) (x)
-#define COL2_ST(x) (x)
-#define COL2_CMUL(a, b) cmul((a), (b))
-#define COL2_CMULC(a, b) cmulc((a), (b))
-#else
-#define COL2_T pk2
-#define COL2_LD(x) to_pk(x)
-#define COL2_ST(x) from_pk(x)
-#define COL2_CMUL(a, b) pk_cmul((a), to_pk(b))
-#define COL2_CMULC(a, b) from_pk(pk_cmulc((a), to_pk(b)))
-#endif
-#ifndef HBX_COL2_ITER
-#define HBX_COL2_ITER 4
-#endif
-template <int R>
-__host__ __device__ constexpr int col2_iters() { return R == 32 ? HBX_COL2_ITER : (R == 16 ? 2 : 1); }
-
-// Second output line without the LDS mirror (default; HBX_COL2_MIRROR keeps the
-// round-1 hand-off for A/B runs): H is even in ky, so
+// forward FFT over y -> Z; Z H and W = Z conj H from the same H(kx, .) row (H
+// is even in fx and fy); inverse FFT of Z H -> B line kx.  H is even in ky, so
 //   IFFT_y(M H)(y) = conj IFFT_y(Z conj H)(y),   M(ky) = conj Z(-ky),
-// i.e. B line N - kx is the conjugate of the inverse FFT of W = Z conj H, which
-// the lanes form in registers from the same H values as Z H.  Only kx = 0 still
-// needs M itself ((Z + M)/2 and (Z - M)/2 are the transforms of the two real
-// lines packed into A line 0): a register shuffle, mirror_conj.
-// HBX_COL2_WPB = 3 builds the pass for three workgroups per CU: float transpose
-// tiles (fft_group_split, 4.2 KB per group) and no next-line prefetch (the
-// third workgroup hides the line loads instead).
-#ifndef HBX_COL2_WPB
-#define HBX_COL2_WPB 2
-#endif
-#ifndef HBX_COL2_PREFETCH
-#define HBX_COL2_PREFETCH (HBX_COL2_WPB < 3)
-#endif
+// i.e. B line N - kx is the conjugate of the inverse FFT of W, formed in
+// registers from the same H values (no LDS mirror).  Only kx = 0 needs M itself
+// ((Z + M)/2 and (Z - M)/2 are the transforms of the two real lines packed into
+// A line 0: a register shuffle, mirror_conj; -> lines 0 and N/2).  One forward
+// FFT per input line, one A read, one H read; every LDS hand-off stays inside
+// the group's own scratch (wave_sync only).  The next line's loads go into v
+// as soon as line kx is stored and fly under the second inverse FFT.
+// Scalar-f32 FFTs: with two lines in registers the packed variant spills.
+// Measured and removed: the round-1 LDS mirror, packed DFTs,
+// three workgroups per CU, H issued ahead, B panels of 8 / 32 / 64 rows.
+template <int R>
+__host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
+
 template <int R, int SK>
-__global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __restrict__ jobs,
+__global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
                                                  const float2* __restrict__ ws_a,
                                                  float2* __restrict__ ws_b,
                                                  const float2* __restrict__ htab,
@@ -398,23 +357,13 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
   constexpr int LB = (N / 2) / (GPB * ITER);
   static_assert((N / 2) % (GPB * ITER) == 0, "line blocking");
   __shared__ float2 tw[N];
+  __shared__ float2 scratch[GPB * R * (R + 1)];
 
   for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
-#if HBX_COL2_WPB > 2
-  __shared__ float scratch[GPB * R * (R + 1)];
-  float* const scf = scratch + grp * R * (R + 1);
-#define COL2_FFT(arr, INV) fft_group_split<R, INV, HBX_COL2_SCALAR>(arr, t, scf, tw)
-#else
-  __shared__ float2 scratch[GPB * R * (R + 1)];
-#define COL2_FFT(arr, INV) fft_group<R, INV, HBX_COL2_SCALAR>(arr, t, sc, tw)
-#endif
-#ifndef HBX_COL2_MIRROR
-  static_assert(HBX_COL2_SCALAR, "the conjugate form keeps the scalar DFT");
   const int lane_base = (threadIdx.x & 63) - t;
-#endif
   int bid = blockIdx.x;
   const int lb = bid % LB;
   bid /= LB;
@@ -428,23 +377,17 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
   // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
-#if HBX_COL2_WPB <= 2
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
-#endif
-#ifdef HBX_COL2_MIRROR
-  static_assert(HBX_COL2_WPB <= 2, "the LDS mirror needs the complex scratch");
-  const float2* mrow = sc.at((R - t) & (R - 1), 0) + (t == 0 ? 1 : 0) + (R - 1);
-#endif
   // the LB blocks of a plane run side by side: at iteration it they hold lines
   // it * LB * GPB + [0, LB * GPB), i.e. whole contiguous stretches of every panel
   constexpr int KSTEP = LB * GPB;
   const int kx0 = lb * GPB + grp;
 
-  COL2_T v[R];
+  float2 v[R];
   {
     const int vo = PA::voff(t, kx0);
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2s(ra, vo, PA::joff(jj)));
+    for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
   }
   lds_barrier();  // tw visible (the line loads stay in flight)
 
@@ -453,29 +396,18 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * N + t) * 8;
-#ifdef HBX_COL2_HEARLY   // A/B switch: the whole H row issued before the forward FFT
-    float2 hall[R];
-#pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) hall[k2] = buf_ld2(rh, vh, k2 * R * 8);
-#define COL2_H(k2) hall[k2]
-#elif defined(HBX_COL2_NOH)   // timing experiment only: no H loads (numerically meaningless)
-#define COL2_H(k2) make_float2(1.0f, 0.0f)
-#else
-#define COL2_H(k2) buf_ld2(rh, vh, (k2) * R * 8)
-#endif
-#ifndef HBX_COL2_MIRROR
-    COL2_FFT(v, false);
-    COL2_T w[R];
+    fft_group<R, false, true>(v, t, sc, tw);
+    float2 w[R];
     if (!dc) {   // v <- Z H, w <- Z conj H, each H value consumed as it arrives
 #pragma unroll
       for (int c8 = 0; c8 < R; c8 += 8) {
         float2 hb[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = COL2_H(c8 + i);
+        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * R * 8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          w[c8 + i] = COL2_CMULC(v[c8 + i], hb[i]);
-          v[c8 + i] = COL2_CMUL(v[c8 + i], hb[i]);
+          w[c8 + i] = cmulc(v[c8 + i], hb[i]);
+          v[c8 + i] = cmul(v[c8 + i], hb[i]);
         }
       }
     } else {     // kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
@@ -485,24 +417,22 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
 #pragma unroll
       for (int k2 = 0; k2 < R; ++k2) {
         const float2 z = v[k2], mm = w[k2];
-        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), COL2_H(k2));
+        v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), buf_ld2(rh, vh, k2 * R * 8));
         w[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * R * 8));
       }
     }
-    COL2_FFT(v, true);
+    fft_group<R, true, true>(v, t, sc, tw);
     {
       const int vo = PB::voff(t, kx);
 #pragma unroll
       for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(v[k2]), rb, vo, PB::joff(k2));
     }
-#if HBX_COL2_PREFETCH
     if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
       const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
       for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
     }
-#endif
-    COL2_FFT(w, true);
+    fft_group<R, true, true>(w, t, sc, tw);
     {
       const int vo = PB::voff(t, dc ? N / 2 : N - kx);
       const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
@@ -510,80 +440,7 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
       for (int k2 = 0; k2 < R; ++k2)
         buf_st2s(store_round<SK>(make_float2(w[k2].x, sy * w[k2].y)), rb, vo, PB::joff(k2));
     }
-#if !HBX_COL2_PREFETCH
-    if (it + 1 < ITER) {
-      const int vo = PA::voff(t, kx + KSTEP);
-#pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
-    }
-#endif
   }
-#else   // HBX_COL2_MIRROR: round-1 form, W through the group's scratch
-#ifdef HBX_COL2_FWD_PACKED   // A/B switch: packed DFTs for the forward FFT only (one line live)
-    fft_group<R, false, false>(v, t, sc, tw);
-#else
-    fft_group<R, false, HBX_COL2_SCALAR>(v, t, sc, tw);
-#endif
-    // W = Z conj(H) (natural order: lane t, register k2 -> ky = t + R k2) goes
-    // to the scratch, plus a pad-slot copy of W[0], while v becomes Z H; then
-    // M H = conj W(N - ky) (H is even in ky) is lane (R - t) mod R, register
-    // R-1-k2, or for lane 0 its own register (R - k2) mod R.  Each H value is
-    // consumed as it arrives, so H never needs a register array of its own.
-    wave_sync();
-    if (!dc) {
-#pragma unroll
-      for (int c8 = 0; c8 < R; c8 += 8) {   // H in batches of 8 loads
-        float2 hb[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = COL2_H(c8 + i);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k2 = c8 + i;
-          const float2 w = COL2_CMULC(v[k2], hb[i]);
-          *sc.at(t, k2) = w;
-          if (k2 == 0) *sc.at(t, R) = w;
-          v[k2] = COL2_CMUL(v[k2], hb[i]);
-        }
-      }
-    } else {  // kx = 0: one group of the whole plane; plain Z through the scratch
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) *sc.at(t, k2) = COL2_ST(v[k2]);
-      *sc.at(t, R) = COL2_ST(v[0]);
-    }
-    wave_sync();
-    COL2_T m[R];
-#pragma unroll
-    for (int k2 = 0; k2 < R; ++k2) m[k2] = COL2_LD(conjf2(mrow[-k2]));
-    if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
-      const int vn = ((N / 2) * N + t) * 8;
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) {
-        const float2 z = COL2_ST(v[k2]), mm = COL2_ST(m[k2]);
-        v[k2] = COL2_LD(cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), COL2_H(k2)));
-        m[k2] = COL2_LD(cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * R * 8)));
-      }
-    }
-    fft_group<R, true, HBX_COL2_SCALAR>(v, t, sc, tw);   // starts with wave_sync: the M reads are done
-    {
-      const int vo = PB::voff(t, kx);
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(COL2_ST(v[k2])), rb, vo, PB::joff(k2));
-    }
-    if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
-      const int vo = PA::voff(t, kx + KSTEP);
-#pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = COL2_LD(buf_ld2s(ra, vo, PA::joff(jj)));
-    }
-    fft_group<R, true, HBX_COL2_SCALAR>(m, t, sc, tw);
-    {
-      const int vo = PB::voff(t, dc ? N / 2 : N - kx);
-#pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(COL2_ST(m[k2])), rb, vo, PB::joff(k2));
-    }
-  }
-#endif
-#undef COL2_H
-#undef COL2_FFT
 }
 
 // ---------------------------------------------------------------------------
@@ -594,7 +451,7 @@ __global__ __launch_bounds__(256, HBX_COL2_WPB) void k_col2(const JobDesc* __res
 template <int R, int GPB>
 __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, const JobDesc& jb, int j, int y,
                                                 int rb, int grp, int t, const float* __restrict__ target,
-                                                size_t tmask, float* __restrict__ inten_out,
+                                                size_t tmask, float* __restrict__ inten_out, int inten_by_env,
                                                 double* __restrict__ partial, double (&red)[GPB][3]) {
   constexpr int N = R * R;
   constexpr int RB = N / GPB;
@@ -613,7 +470,8 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
     acc[k] = I;
   }
   if (inten_out) {
-    float* orow = inten_out + ((size_t)j * N + y) * N;
+    const size_t slot = inten_by_env ? (size_t)jb.env * G + jb.group : (size_t)j;
+    float* orow = inten_out + (slot * N + y) * N;
 #pragma unroll
     for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
   }
@@ -642,7 +500,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
                                                    int G, double* __restrict__ partial,
                                                    float* __restrict__ inten_out,
                                                    float2* __restrict__ field_out,
-                                                   size_t tmask) {
+                                                   size_t tmask, int inten_by_env) {
   constexpr int N = R * R;
   constexpr int GPB = NT / R;          // rows per block
   constexpr int RB = N / GPB;
@@ -719,7 +577,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowinv(const JobDesc* __restri
     }
   }
 
-  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, partial, red);
+  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -867,19 +725,13 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   const int P = pd.P;
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
-  if (R == 32 && pd.colbits) {   // bits -> B without the A intermediate (hbx_colbits.hip)
-    const hipError_t e = launch_colbits(pd, jobs, n_jobs, mask, st);
-    if (e != hipSuccess) return e;
-  } else {
   {
     const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
     if (tm) tm->begin(0, st);
-#ifndef HBX_ROWFWD_WIDE   // A/B switch: `make exp EXP=ROWFWD_WIDE` keeps the two-block kernel
-    if constexpr (R == 32 && kRowNT<R> == 256)
+    if constexpr (R == 32)
       hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
                          pd.va, pd.vb);
     else
-#endif
     hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
                        CH, pd.va, pd.vb);
     if (tm) tm->end(0, n_jobs, st);
@@ -891,13 +743,12 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     hipLaunchKernelGGL((k_col2<R, SK>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
     if (tm) tm->end(1, n_jobs, st);
   }
-  }
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
     hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                        target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
-                       field_out, target ? ~(size_t)0 : (size_t)0);
+                       field_out, target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
     if (tm) tm->end(2, n_jobs, st);
   }
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial,
@@ -907,10 +758,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
 
 hipError_t run_jobs(const PlanDev& pd, const JobDesc* jobs, int n_jobs, const uint32_t* mask,
                     const float* target, float* inten_out, float2* field_out, hipStream_t st) {
-  if (pd.R == 0 && pd.fused896) return run_jobs_896(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
-  if (pd.R == 0)
-    return run_jobs_generic(pd, jobs, n_jobs, reinterpret_cast<const uint64_t*>(mask), target, inten_out,
-                            field_out, st);
+  if (pd.R == 0) return run_jobs_896(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);
   switch (pd.R * 4 + pd.store_kind) {
 #define HBX_PASSES_CASE(R_, SK_) \
     case R_ * 4 + SK_: return launch_passes<R_, SK_>(pd, jobs, n_jobs, mask, target, inten_out, field_out, st);

@@ -18,9 +18,9 @@
 //                rows (next plane prefetched) -> IFFT over kx -> |U|^2 -> plane
 //                mean -> f64 partials of (I T, I^2, T^2)  [read 8 N^2 per plane + 4 N^2]
 //
-// A is [kx < 448][y], B is [kx < 896][y] (column-major lines).  It replaces
-// the composed path of hbx_generic.hip (kept behind HBX_GENERIC896=1), which
-// moved ~10 plane-sized round trips per job instead of 3.
+// A is [kx < 448][y], B is [kx < 896][y] (column-major lines).  It replaced
+// a composed path (2-D FFTs around a transfer-function pass, removed in r03),
+// which moved ~10 plane-sized round trips per job instead of 3.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -159,16 +159,8 @@ __global__ __launch_bounds__(256, 2) void k_rowfwd896(const JobDesc* __restrict_
 // (H is even in ky); IFFT of Z H -> B line kx, of M H -> B line N - kx
 // (kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448)
 // ---------------------------------------------------------------------------
-#ifndef HBX_896_COL_PACKED
 constexpr bool kColScalar = true;    // packed 32-point DFTs spill with two lines live
-#else
-constexpr bool kColScalar = false;
-#endif
-#ifdef HBX_896_INV_SCALAR
-constexpr bool kInvScalar = true;
-#else
-constexpr bool kInvScalar = false;
-#endif
+constexpr bool kInvScalar = false;   // k_rowinv896: packed DFTs (one line live)
 constexpr int kColIter = 4;
 constexpr int kColLB = kHalf / (kGPB * kColIter);   // 14 blocks per plane
 static_assert(kHalf % (kGPB * kColIter) == 0, "line blocking");
@@ -282,14 +274,12 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
                                                       const float2* __restrict__ tw_glob, int P, int G,
                                                       double* __restrict__ partial,
                                                       float* __restrict__ inten_out,
-                                                      float2* __restrict__ field_out, size_t tmask) {
+                                                      float2* __restrict__ field_out, size_t tmask,
+                                                      int inten_by_env) {
   constexpr int CH16 = kN * kGPB / 2;   // 16-B chunks per plane tile
   constexpr int PER = CH16 / 256;
   static_assert(CH16 % 256 == 0, "chunking");
-#ifndef HBX_896_INV_PF
-#define HBX_896_INV_PF 8
-#endif
-  constexpr int PF = HBX_896_INV_PF < PER ? HBX_896_INV_PF : PER;
+  constexpr int PF = 8 < PER ? 8 : PER;   // chunks prefetched a plane ahead (all of them spilled)
   __shared__ float2 tw[kN];
   __shared__ __attribute__((aligned(16))) float2 tile[kSCR];
   __shared__ double red[kGPB][3];
@@ -384,7 +374,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
     acc[k] = I;
   }
   if (inten_out) {
-    float* orow = inten_out + ((size_t)j * kN + y) * kN;
+    const size_t slot = inten_by_env ? (size_t)jb.env * G + jb.group : (size_t)j;
+    float* orow = inten_out + (slot * kN + y) * kN;
 #pragma unroll
     for (int k = 0; k < kL; ++k) orow[t + kR * k] = acc[k];
   }
@@ -423,7 +414,7 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
   if (tm) tm->begin(2, st);
   hipLaunchKernelGGL(k_rowinv896, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
                      target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
-                     target ? ~(size_t)0 : (size_t)0);
+                     target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
   if (tm) tm->end(2, n_jobs, st);
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial, n_jobs, kRB,
                      pd.job_stats);

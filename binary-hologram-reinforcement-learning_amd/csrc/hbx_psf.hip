@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_psf_order(JobDesc* __restrict__ jobs, i
   }
 }
 
-// grid (kPsfBlocks, n_jobs); each thread walks single pixels (HBX_PSF_QUAD: quads of 4 consecutive pixels)
+// grid (kPsfBlocks, n_jobs); each thread walks single pixels
 __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jobs,
                                                   const int32_t* __restrict__ order,
                                                   const uint64_t* __restrict__ mask,
@@ -149,12 +149,9 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
     const float delta = flip_delta(mask, jb, N, P, CH, vb, false);
     const float invp = 1.0f / (float)P;
     const size_t hw = (size_t)N * N;
-    const float4* U = reinterpret_cast<const float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
-    const float4* I = reinterpret_cast<const float4*>(inten + ((size_t)jb.env * G + g) * hw);
-    const float4* T = reinterpret_cast<const float4*>(target + ((size_t)jb.env * G + g) * hw);
     const float2* h = hpsf + (size_t)g * hw;
-#ifndef HBX_PSF_QUAD   // one pixel per lane: the shifted h reads coalesce per wave (measured 0.457 -> 0.445 and 0.427 -> 0.419 ms
-                       // per 128-job launch vs four pixels per lane, `make exp EXP=PSF_QUAD`; tools/psf_ab.sh)
+    // one pixel per lane: the shifted h reads coalesce per wave (measured 0.457 -> 0.445 and
+    // 0.427 -> 0.419 ms per 128-job launch against four pixels per lane, r01)
     const float2* U2 = field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw;
     const float* I1 = inten + ((size_t)jb.env * G + g) * hw;
     const float* T1 = target + ((size_t)jb.env * G + g) * hw;
@@ -163,7 +160,7 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
     for (int q = blockIdx.x * 256 + threadIdx.x; q < npx; q += kPsfBlocks * 256) {
       const int y = q / N, x = q % N;
       // the once-read streams are non-temporal, so they do not push h_g out of the L2:
-      // measured 0.409 -> 0.367 ms per 128-job launch (tools/psf_ab.sh)
+      // measured 0.409 -> 0.367 ms per 128-job launch
       typedef float f2v __attribute__((ext_vector_type(2)));
       const f2v uv = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(U2 + q));
       const float2 u = make_float2(uv.x, uv.y);
@@ -172,26 +169,6 @@ __global__ __launch_bounds__(256) void k_psf_eval(const JobDesc* __restrict__ jo
       const float dI = flip_dI(u.x, u.y, hv.x, hv.y, delta, invp);
       sxy = fma((double)dI, (double)tv, sxy);
       sxx = fma((double)fmaf(2.0f, iv, dI), (double)dI, sxx);
-    }
-    if (false)
-#endif
-    for (int q = blockIdx.x * 256 + threadIdx.x; q < (int)(hw / 4); q += kPsfBlocks * 256) {
-      const int y = (4 * q) / N, x0 = (4 * q) % N;
-      const float4 u01 = U[2 * q], u23 = U[2 * q + 1];
-      const float4 iv = I[q], tv = T[q];
-      const float2* hrow = h + (size_t)fold(y - r, N) * N;
-      const float2 h0 = hrow[fold(x0 - col, N)], h1 = hrow[fold(x0 + 1 - col, N)];
-      const float2 h2 = hrow[fold(x0 + 2 - col, N)], h3 = hrow[fold(x0 + 3 - col, N)];
-      const float uu[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
-      const float hh[8] = {h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
-      const float ii[4] = {iv.x, iv.y, iv.z, iv.w};
-      const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float dI = flip_dI(uu[2 * k], uu[2 * k + 1], hh[2 * k], hh[2 * k + 1], delta, invp);
-        sxy = fma((double)dI, (double)tt[k], sxy);
-        sxx = fma((double)fmaf(2.0f, ii[k], dI), (double)dI, sxx);
-      }
     }
   }
   block_sum2<256>(sxy, sxx, red);
@@ -254,14 +231,11 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
   const float delta = flip_delta(mask, jb, N, P, CH, vb, true);
   const float invp = 1.0f / (float)P;
   const size_t hw = (size_t)N * N;
-  float4* U = reinterpret_cast<float4*>(field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw);
-  float4* I = reinterpret_cast<float4*>(inten + ((size_t)jb.env * G + g) * hw);
   const float2* h = hpsf + (size_t)g * hw;
-#ifndef HBX_PSF_COMMIT_QUAD   // one pixel per lane, as k_psf_eval (coalesced shifted-h reads): 0.292 -> 0.287 ms
-                             // per 128-job step against four pixels per lane (`make exp EXP=PSF_COMMIT_QUAD`,
-                             // profiles/r02/psf_commit_px1_ab.txt)
-  float2* U2 = reinterpret_cast<float2*>(U);
-  float* I1 = reinterpret_cast<float*>(I);
+  // one pixel per lane, as k_psf_eval (coalesced shifted-h reads): 0.292 -> 0.287 ms per
+  // 128-job step against four pixels per lane (profiles/r02/psf_commit_px1_ab.txt)
+  float2* U2 = field + ((size_t)jb.env * CH + g * P + jb.flip_plane) * hw;
+  float* I1 = inten + ((size_t)jb.env * G + g) * hw;
 #pragma unroll 4
   for (int q = blockIdx.x * 256 + threadIdx.x; q < (int)hw; q += kPsfBlocks * 256) {
     const int y = q / N, x = q % N;
@@ -273,30 +247,6 @@ __global__ __launch_bounds__(256) void k_psf_commit(const JobDesc* __restrict__ 
     u.y = fmaf(delta, hv.y, u.y);
     U2[q] = u;
     I1[q] = iv;
-  }
-  return;
-#endif
-  const int nq = (int)(hw / 4);
-  for (int q = blockIdx.x * 256 + threadIdx.x; q < nq; q += kPsfBlocks * 256) {
-    const int y = (4 * q) / N, x0 = (4 * q) % N;
-    float4 u01 = U[2 * q], u23 = U[2 * q + 1];
-    float4 iv = I[q];
-    const float2* hrow = h + (size_t)fold(y - r, N) * N;
-    const float2 h0 = hrow[fold(x0 - col, N)], h1 = hrow[fold(x0 + 1 - col, N)];
-    const float2 h2 = hrow[fold(x0 + 2 - col, N)], h3 = hrow[fold(x0 + 3 - col, N)];
-    float uu[8] = {u01.x, u01.y, u01.z, u01.w, u23.x, u23.y, u23.z, u23.w};
-    const float hh[8] = {h0.x, h0.y, h1.x, h1.y, h2.x, h2.y, h3.x, h3.y};
-    float ii[4] = {iv.x, iv.y, iv.z, iv.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float ur = uu[2 * k], ui = uu[2 * k + 1];
-      ii[k] += flip_dI(ur, ui, hh[2 * k], hh[2 * k + 1], delta, invp);
-      uu[2 * k] = fmaf(delta, hh[2 * k], ur);
-      uu[2 * k + 1] = fmaf(delta, hh[2 * k + 1], ui);
-    }
-    U[2 * q] = make_float4(uu[0], uu[1], uu[2], uu[3]);
-    U[2 * q + 1] = make_float4(uu[4], uu[5], uu[6], uu[7]);
-    I[q] = make_float4(ii[0], ii[1], ii[2], ii[3]);
   }
 }
 

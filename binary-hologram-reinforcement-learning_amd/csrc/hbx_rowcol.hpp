@@ -54,43 +54,17 @@ __device__ __forceinline__ void buf_st2(float2 v, __amdgpu_buffer_rsrc_t rs, int
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
 
-// Cache policy of the once-touched intermediate streams (A, B): timing switches
-// HBX_NT_LOADS / HBX_NT_STORES set the non-temporal bit (buffer aux = 2,
-// `__builtin_nontemporal_*` for flat accesses).
-#ifdef HBX_NT_LOADS
-constexpr int kLdAux = 2;
-#else
-constexpr int kLdAux = 0;
-#endif
-#ifdef HBX_NT_STORES
-constexpr int kStAux = 2;
-#else
-constexpr int kStAux = 0;
-#endif
+// The once-touched intermediate streams (A, B) keep the default cache policy:
+// non-temporal loads slowed k_rowinv 1.80 -> 2.21 ms and non-temporal stores
+// k_rowfwd 1.17 -> 1.27 ms.
 __device__ __forceinline__ float2 buf_ld2s(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, kLdAux));
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
 }
 __device__ __forceinline__ void buf_st2s(float2 v, __amdgpu_buffer_rsrc_t rs, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, kStAux);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
-__device__ __forceinline__ float4 ld_stream4(const float2* p) {
-#ifdef HBX_NT_LOADS
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-#else
-  return *reinterpret_cast<const float4*>(p);
-#endif
-}
-__device__ __forceinline__ void st_stream4(float2* p, float4 v) {
-#ifdef HBX_NT_STORES
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v w = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
-#else
-  *reinterpret_cast<float4*>(p) = v;
-#endif
-}
+__device__ __forceinline__ float4 ld_stream4(const float2* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st_stream4(float2* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 // Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
 // the 8 XCDs; placement is a speed hint only, never relied on for
@@ -99,12 +73,10 @@ __device__ __forceinline__ void st_stream4(float2* p, float4 v) {
 // line is read / written as GS*64 contiguous bytes through one L2.  Measured
 // on 1024x24, 128 envs (k_rowfwd / k_rowinv ms): no remap 1.34 / 2.75,
 // GS=2 1.18 / 2.43, GS=4 1.17 / 2.40, GS=8 1.12 / 2.08, GS=16 1.12 / 1.98.
-#ifndef HBX_XCD_GROUP
-#define HBX_XCD_GROUP 16
-#endif
+constexpr int kXcdGroup = 16;
 template <int RB>
 __device__ __forceinline__ int xcd_pair(int bid) {
-  constexpr int GS = (RB / 8 < HBX_XCD_GROUP) ? RB / 8 : HBX_XCD_GROUP;
+  constexpr int GS = (RB / 8 < kXcdGroup) ? RB / 8 : kXcdGroup;
   constexpr int SPAN = 8 * (GS > 0 ? GS : 1);
   if constexpr (GS > 1 && RB % SPAN == 0)
     return (bid / SPAN) * SPAN + (bid % 8) * GS + (bid / 8) % GS;

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 7
+ABI_VERSION = 8
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -25,6 +25,7 @@ MAX_GROUPS = 4
 WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
 WALK_FUSED_K = (1, 2, 3, 4)   # one launch per batch (two accepts resolved for K = 2..4)
 PRECISION_F32, PRECISION_BF16_STORE, PRECISION_F16_STORE = 0, 1, 2   # hbx_plan_set_precision
+OBS_STATE, OBS_RECON = 1, 2   # hbx_env_obs_sync
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
@@ -32,15 +33,14 @@ EXPORTED_SYMBOLS = (
     "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
-    "hbx_plan_set_precision", "hbx_plan_precision",
+    "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
-# kernels in the ROWFWD / COL timer slots per pipeline (hbx_plan_pipeline)
-PIPE_THREE_PASS, PIPE_COLBITS, PIPE_GENERIC = 0, 1, 2
-PIPE_PASS_NAMES = {PIPE_THREE_PASS: PASS_NAMES,
-                   PIPE_COLBITS: ("k_bits_t", "k_colbits", "k_rowinv", "k_psf_eval", "k_psf_commit"),
-                   PIPE_GENERIC: PASS_NAMES}
+# hbx_plan_pipeline: the three-pass pipeline is the only one built since ABI v8 (the
+# bits -> column and composed-896 variants measured slower and were removed)
+PIPE_THREE_PASS = 0
+PIPE_PASS_NAMES = {PIPE_THREE_PASS: PASS_NAMES}
 
 
 class HbxError(RuntimeError):
@@ -81,6 +81,7 @@ class EnvBuffers(C.Structure):
         ("field", C.c_void_p),
         ("imp_changes", C.c_void_p), ("imp_values", C.c_void_p), ("t_psnr_diff", C.c_void_p),
         ("imp_count", C.c_int32), ("reserved", C.c_int32),
+        ("state_bytes", C.c_void_p), ("recon", C.c_void_p), ("recon_pending", C.c_void_p),
     ]
 
 
@@ -123,6 +124,7 @@ def _declare(lib):
     lib.hbx_dbs_walk_psf.argtypes = [VP, VP, VP, VP, VP, VP, VP, I64, VP, VP, VP, I64, I32, I32, VP]
     lib.hbx_plan_set_precision.argtypes = [VP, I32]
     lib.hbx_plan_precision.argtypes = [VP]
+    lib.hbx_env_obs_sync.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, I32, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]

@@ -116,9 +116,7 @@ def greedy_dataset(n_images: int, load, order_for, plan_factory, per_gpu: int = 
     buf = torch.full((per_rank, 8), -1.0, dtype=torch.float64)
     if rows:
         buf[:len(rows)] = torch.tensor(rows, dtype=torch.float64)
-    if world > 1 and tdist.get_backend() == "nccl":
-        buf = buf.to(torch.device("cuda", torch.cuda.current_device()))
-    got = hd.gather_to_rank0(buf)
+    got = hd.gather_to_rank0(buf)        # RCCL / gloo whenever a group exists (any world size)
     if got is None:
         return None
     keys = ("image", "initial_psnr", "final_psnr", "candidates", "accepted", "seconds", "stopped_early", "rank")
@@ -662,10 +660,9 @@ def probe_sharded(plan: Plan, mask: torch.Tensor, target: torch.Tensor, flips, p
         rank, world = torch.distributed.get_rank(), torch.distributed.get_world_size()
     lo, hi = hd.shard_range(len(flips), rank, world)
     res = probe(plan, mask, target, flips[lo:hi], pre_model=pre_model, stream=stream)
-    # histogram rows + improved count in one f64 all-reduce (device of the collective's backend)
-    backend = torch.distributed.get_backend() if world > 1 else "gloo"
-    dev = plan.device if backend == "nccl" else torch.device("cpu")
-    buf = torch.zeros(31, dtype=torch.float64, device=dev)
+    # histogram rows + improved count in one f64 all-reduce (device of the collective's backend;
+    # runs whenever a process group exists, world 1 included)
+    buf = torch.zeros(31, dtype=torch.float64, device=hd.collective_device(plan.device))
     buf[0:10] = torch.as_tensor(res.attempted_bins, dtype=torch.float64)
     buf[10:20] = torch.as_tensor(res.improved_bins, dtype=torch.float64)
     buf[20:30] = torch.as_tensor(res.delta_bins, dtype=torch.float64)

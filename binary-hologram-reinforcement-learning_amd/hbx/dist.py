@@ -4,6 +4,11 @@ SURVEY 8e: env instances shard with no exchange on the compute path; the
 only collective is a small gather of rewards / psnr / done flags to rank 0
 (torch.distributed, backend "nccl" = RCCL over xGMI on ROCm; "gloo" in CPU
 tests).  Probe sweeps shard the flip range and all-reduce a 10-bin histogram.
+
+Every collective here runs whenever a process group exists, including a
+world of one: ``init(force=True)`` (or ``HBX_DIST_FORCE_PG=1``) builds that
+group without a launcher, so a one-GPU run executes the same RCCL calls as
+the 8-GPU one (train-PPO.py:296-322's caller, BASELINE configs[3]).
 """
 from __future__ import annotations
 
@@ -21,19 +26,55 @@ def env_rank_world() -> Tuple[int, int, int]:
     return rank, world, local
 
 
-def init(backend: Optional[str] = None) -> Tuple[int, int, int]:
-    """Initialise the default process group from torchrun's env vars (no-op at world 1)."""
+def active() -> bool:
+    """A process group exists (any world size): the collectives below run."""
+    return dist.is_available() and dist.is_initialized()
+
+
+def init(backend: Optional[str] = None, force: Optional[bool] = None) -> Tuple[int, int, int]:
+    """Initialise the default process group from torchrun's env vars.
+
+    World > 1 always builds the group.  At world 1 the group is built only when
+    ``force`` (default: ``HBX_DIST_FORCE_PG=1`` in the environment); without
+    torchrun's MASTER_PORT it rendezvouses through an in-process HashStore.
+    backend None -> "nccl" (RCCL) when a GPU is visible, else "gloo".  The nccl
+    group is bound to cuda:LOCAL_RANK (device_id), so its communicator is
+    created eagerly here -- before any other GPU work of the caller."""
     rank, world, local = env_rank_world()
-    if world > 1 and not dist.is_initialized():
+    if force is None:
+        force = os.environ.get("HBX_DIST_FORCE_PG") == "1"
+    if active() or not (world > 1 or force):
+        return rank, world, local
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    if world == 1 and "MASTER_PORT" not in os.environ:
+        dist.init_process_group(backend, store=dist.HashStore(), rank=0, world_size=1, **kw)
+    else:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group(backend, **kw)
     return rank, world, local
+
+
+def shutdown():
+    if active():
+        dist.destroy_process_group()
+
+
+def backend() -> str:
+    return dist.get_backend() if active() else "none"
+
+
+def collective_device(home: Optional[torch.device] = None) -> torch.device:
+    """Where the backend's collectives take their tensors: the current GPU for
+    nccl (RCCL), the host for gloo."""
+    if backend() == "nccl":
+        return home if home is not None and home.type == "cuda" else \
+            torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
 def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
@@ -46,13 +87,11 @@ def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
 def gather_to_rank0(t: torch.Tensor) -> Optional[torch.Tensor]:
     """Concatenate equal-shaped per-rank tensors on rank 0 (None elsewhere):
     one dist.gather, so only rank 0 receives (RCCL send/recv to the root over
-    xGMI; gloo on CPU)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    xGMI; gloo on CPU).  Without a process group: t itself."""
+    if not active():
         return t
     home = t.device
-    t = t.contiguous()
-    if dist.get_backend() == "gloo" and t.is_cuda:   # gloo's gather takes host tensors
-        t = t.cpu()
+    t = t.contiguous().to(collective_device(home))
     if dist.get_rank() == 0:
         parts: List[torch.Tensor] = [torch.empty_like(t) for _ in range(dist.get_world_size())]
         dist.gather(t, gather_list=parts, dst=0)
@@ -87,21 +126,27 @@ class StepMetricGather:
         out = gather_to_rank0(self.buf[:self.n])
         self.n = 0
         if out is not None:
+            # the gather may return the buffer itself (no group): keep a copy, the
+            # buffer is overwritten by the next steps
+            out = out.clone() if out.data_ptr() == self.buf.data_ptr() else out
             self.gathered.append(out)
         return out
 
 
 def describe_world(device=None) -> List[List]:
     """[rank, world, local_rank, backend] as every rank saw it, gathered to rank 0
-    (the bench prints it so a multi-GPU line is self-checking)."""
+    over the group's own backend (the bench prints it so a multi-GPU line is
+    self-checking)."""
     rank, world, local = env_rank_world()
-    backend = dist.get_backend() if dist.is_initialized() else "none"
+    if active():
+        rank, world = dist.get_rank(), dist.get_world_size()
+    be = backend()
     row = torch.tensor([rank, world, local], dtype=torch.int64,
-                       device=device if backend == "nccl" else "cpu")
+                       device=collective_device(torch.device(device) if device is not None else None))
     allr = gather_to_rank0(row.unsqueeze(0))
     if allr is None:
         return []
-    return [[int(a), int(b), int(c), backend] for a, b, c in allr.cpu().tolist()]
+    return [[int(a), int(b), int(c), be] for a, b, c in allr.cpu().tolist()]
 
 
 def pack_step_metrics(reward: torch.Tensor, psnr: torch.Tensor, accepted: torch.Tensor,
@@ -112,19 +157,29 @@ def pack_step_metrics(reward: torch.Tensor, psnr: torch.Tensor, accepted: torch.
 
 
 def allreduce_hist(counts: torch.Tensor) -> torch.Tensor:
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    """Sum `counts` over the ranks in place (on the backend's device; the result
+    is copied back when `counts` lives elsewhere)."""
+    if not active():
+        return counts
+    dev = collective_device(counts.device)
+    if counts.device == dev:
         dist.all_reduce(counts)
+        return counts
+    t = counts.to(dev)
+    dist.all_reduce(t)
+    counts.copy_(t)
     return counts
 
 
 def max_over_ranks(x: float, device: Optional[torch.device] = None) -> float:
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    if not active():
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=device)
+    t = torch.tensor([x], dtype=torch.float64,
+                     device=collective_device(torch.device(device) if device is not None else None))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier():
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if active():
         dist.barrier()

@@ -82,10 +82,18 @@ class EnvState:
     """Device buffers of B environments (env.py:65-81 attributes)."""
 
     def __init__(self, plan: Plan, n_env: int, keep_record: bool = True, keep_pre_model: bool = True,
-                 keep_intensity: bool = True, keep_field: bool = False, importance_samples: int = 0):
+                 keep_intensity: bool = True, keep_field: bool = False, importance_samples: int = 0,
+                 keep_state_bytes: bool = False, keep_recon: bool = False):
         c, dev = plan.cfg, plan.device
         self.plan, self.n = plan, n_env
-        keep_intensity = keep_intensity or keep_field   # the incremental mode needs both
+        keep_intensity = keep_intensity or keep_field or keep_recon   # the incremental mode / recon need it
+        # zero-copy observations (ABI v8): obs["state"] as int8 0/1 (env.py:177 hands out
+        # self.state), obs["recon_image"] with the stepped group's pre-rollback intensity
+        # (env.py:179); both kept current by the reset / step kernels
+        self.state_bytes = torch.zeros((n_env, c.channels, c.height, c.width), dtype=torch.int8,
+                                       device=dev) if keep_state_bytes else None
+        self.recon = torch.zeros(plan.target_shape(n_env), dtype=torch.float32, device=dev) if keep_recon else None
+        self.recon_pending = torch.zeros(n_env, dtype=torch.int32, device=dev) if keep_recon else None
         # complex64 field of every plane, as float32 pairs (incremental-field mode)
         self.field = torch.zeros((n_env, c.channels, c.height, c.width, 2), dtype=torch.float32,
                                  device=dev) if keep_field else None
@@ -122,6 +130,7 @@ class EnvState:
         b.field = p(self.field)
         b.imp_changes, b.imp_values, b.t_psnr_diff = p(self.imp_changes), p(self.imp_values), p(self.t_psnr_diff)
         b.imp_count = k
+        b.state_bytes, b.recon, b.recon_pending = p(self.state_bytes), p(self.recon), p(self.recon_pending)
 
     def check_error(self):
         if int(self.error.item()) != 0:
@@ -202,9 +211,11 @@ class HologramVecEnv(_VecEnvBase):
         self.state = EnvState(self.plan, self.num_envs,
                               keep_record=True,
                               keep_pre_model="pre_model" in self.obs_keys,
-                              keep_intensity="recon_image" in self.obs_keys,
+                              keep_intensity=False,
                               keep_field=(mode == "psf"),
-                              importance_samples=self.importance_samples)
+                              importance_samples=self.importance_samples,
+                              keep_state_bytes="state" in self.obs_keys,
+                              keep_recon="recon_image" in self.obs_keys)
         self.target_source = target_source
         self.pre_model_fn = pre_model_fn
         self.pre_model_source = pre_model_source
@@ -239,8 +250,6 @@ class HologramVecEnv(_VecEnvBase):
         self._acc = torch.zeros(n, dtype=torch.uint8, device=dev)
         self._term = torch.zeros(n, dtype=torch.uint8, device=dev)
         self._trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self._ginten = torch.zeros((n, c.height, c.width), dtype=torch.float32, device=dev) \
-            if "recon_image" in self.obs_keys else None
         self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
         self.episode_count = 0
@@ -301,8 +310,6 @@ class HologramVecEnv(_VecEnvBase):
         Seeds given through seed() are recorded and consumed here (the reference
         ignores reset's seed, env.py:90 -- SURVEY F9)."""
         self.reset_envs(range(self.num_envs))
-        if self._ginten is not None and self.state.intensity is not None:
-            self._ginten.zero_()
         self._seeds = [None for _ in range(self.num_envs)]
         self.reset_infos = [{} for _ in range(self.num_envs)]
         return self._format(self.observe(stepped=False))
@@ -346,7 +353,7 @@ class HologramVecEnv(_VecEnvBase):
                 self.refresh()
         else:
             self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, self._reward,
-                               self._psnr, self._acc, self._term, self._trunc, self._ginten)
+                               self._psnr, self._acc, self._term, self._trunc)
         return self._reward, self._psnr, self._acc, self._term, self._trunc
 
     def refresh(self):
@@ -359,13 +366,17 @@ class HologramVecEnv(_VecEnvBase):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
         (done envs report their last observation as info["terminal_observation"])."""
         reward, psnr, acc, term, trunc = self.step_device(actions)
-        self.state.check_error()
+        n = self.num_envs
+        # one device -> host copy per step: rewards, done flags and the error word together
+        host = torch.cat([reward, term.double(), trunc.double(), self.state.error.double()]).cpu().numpy()
+        if host[3 * n] != 0:
+            self.state.check_error()                      # clears the word and raises
         obs = self.observe(stepped=True)
-        r = reward.cpu().numpy()
+        r = host[:n].copy()
         if self.obs_format != "torch":
             r = r.astype(np.float32)
-        t = term.cpu().numpy().astype(bool)
-        tr = trunc.cpu().numpy().astype(bool)
+        t = host[n:2 * n] != 0
+        tr = host[2 * n:3 * n] != 0
         dones = t | tr
         infos = [{} for _ in range(self.num_envs)]
         if self.auto_reset and dones.any():
@@ -459,34 +470,41 @@ class HologramVecEnv(_VecEnvBase):
         return self
 
     def getattr_depth_check(self, name, already_found):
-        return self if hasattr(self, name) and already_found else None
+        """SB3 VecEnv contract: the wrapper's class name when `name` would be found
+        here and already_found, else None (used in VecEnvWrapper error messages)."""
+        if hasattr(self, name) and already_found:
+            return f"{type(self).__module__}.{type(self).__name__}"
+        return None
 
     # -- observations (env.py:135-140,176-181) ----------------------------------------
-    def observe(self, stepped: bool):
-        st, c = self.state, self.cfg
+    def observe(self, stepped: bool = True):
+        """The batched observation dict: every value is a VIEW of the env state the
+        kernels keep current (no copy, as env.py:176-181 hands out self.state and its
+        other arrays) -- state_record / state / pre_model (B, 1, CH, N, N), recon_image /
+        target_image (B, 1, G, N, N).  After a step, recon_image's stepped group is the
+        stepped (pre-rollback) reconstruction (env.py:179), the other groups the cached
+        accepted ones; after a reset it is the reset state's.  The views change with the
+        next step: a consumer that keeps an observation copies it (SB3's rollout buffers
+        do).  `stepped` is accepted for callers of the r02 signature."""
+        st = self.state
         out = {}
         for k in self.obs_keys:
             if k == "state_record":
                 out[k] = st.record.unsqueeze(1)
             elif k == "state":
-                out[k] = unpack_bits(st.mask, c.width).unsqueeze(1)
+                out[k] = st.state_bytes.unsqueeze(1)
             elif k == "pre_model":
                 out[k] = st.pre_model.unsqueeze(1)
             elif k == "target_image":
                 out[k] = st.target.unsqueeze(1)
             elif k == "recon_image":
-                rec = st.intensity.clone()
-                if stepped and self._ginten is not None:
-                    # the reference returns the stepped (pre-rollback) recon (env.py:179)
-                    g = (self._last_actions // (c.height * c.width)) // c.planes
-                    rec[torch.arange(self.num_envs, device=self.device), g] = self._ginten
-                out[k] = rec.unsqueeze(1)
+                out[k] = st.recon.unsqueeze(1)
         return out
 
     # -- checkpoint / resume (SURVEY 5: the env state is plain tensors) ---------------
     _SNAPSHOT = ("mask", "record", "target", "pre_model", "intensity", "chan_stats", "init_psnr",
                  "prev_psnr", "max_psnr_diff", "steps", "flip_count", "sustained", "imp_changes",
-                 "imp_values", "t_psnr_diff")
+                 "imp_values", "t_psnr_diff", "recon", "recon_pending")
 
     def save(self, path: str):
         """Every env's device state to an .npz (bit-packed masks, records, targets,
@@ -508,12 +526,19 @@ class HologramVecEnv(_VecEnvBase):
             if meta != (c.height, c.width, c.groups, c.planes, self.num_envs):
                 raise ValueError(f"snapshot shape {meta} does not match this env "
                                  f"{(c.height, c.width, c.groups, c.planes, self.num_envs)}")
+            have_recon = "recon" in z.files and "recon_pending" in z.files
             for k in self._SNAPSHOT:
                 t = getattr(st, k)
                 if t is not None and k in z.files:
                     t.copy_(torch.from_numpy(z[k]))
         if self.mode == "psf":
             self.refresh()
+        # obs["state"] follows the restored mask; recon from the intensity cache when the
+        # snapshot holds no recon of its own
+        what = (_lib.OBS_STATE if st.state_bytes is not None else 0) | \
+               (_lib.OBS_RECON if st.recon is not None and not have_recon else 0)
+        if what:
+            self.plan.env_obs_sync(st.bufs, self.num_envs, what)
 
     # -- gym-ish accessors ------------------------------------------------------------
     @property
@@ -554,7 +579,8 @@ class BinaryHologramEnv(spaces.EnvBase):
     (env.py:135-140,176-181) -- and ``observation_space.contains`` accepts them;
     scalars are Python floats.
 
-    verbose=True prints the reference's console lines (env.py:100,104,142-145:
+    verbose=True (the default, as the reference always prints) gives the reference's
+    console lines (env.py:100,104,142-145:
     episode start, initial PSNR / MSE; :203-246: a Step block at every 0.01 dB
     threshold, at the T_PSNR_DIFF condition and at max_steps).  debug_timing=True
     adds debug_env.py's per-phase lines (`Step: N | Time <phase>: s seconds`,
@@ -563,7 +589,7 @@ class BinaryHologramEnv(spaces.EnvBase):
     of every propagation pass (hbx_plan_read_timing)."""
 
     def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
-                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = True,
                  device: Optional[int] = None, debug_timing: bool = False, **vec_kwargs):
         super().__init__()
         self.cfg = config or mono_config(256)
@@ -611,7 +637,9 @@ class BinaryHologramEnv(spaces.EnvBase):
 
     @property
     def state(self):
-        return unpack_bits(self._vec.state.mask[0], self.cfg.width).unsqueeze(0).cpu().numpy()
+        sb = self._vec.state.state_bytes
+        bits = sb[0] if sb is not None else unpack_bits(self._vec.state.mask[0], self.cfg.width)
+        return bits.unsqueeze(0).cpu().numpy()
 
     def _obs(self, stepped: bool) -> dict:
         """The B = 1 batch axis of HologramVecEnv.observe() removed: (1, CH, N, N) /
@@ -731,7 +759,7 @@ class BinaryHologramEnvGroup(BinaryHologramEnv):
     like the reference's attributes (env_group.py:186-198)."""
 
     def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
-                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = True,
                  device: Optional[int] = None, importance_samples: int = 10000, importance_seed: int = 0):
         super().__init__(target_function, trainloader, max_steps=max_steps, T_PSNR=T_PSNR, T_steps=T_steps,
                          T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device,
@@ -757,7 +785,7 @@ class BinaryHologramEnvMD(BinaryHologramEnv):
     (env_md.py:54,156-160)."""
 
     def __init__(self, target_function, trainloader, max_steps=10000, T_PSNR=30, T_steps=1,
-                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = False,
+                 T_PSNR_DIFF=0.1, config: Optional[OpticsConfig] = None, verbose: bool = True,
                  device: Optional[int] = None):
         super().__init__(target_function, trainloader, max_steps=max_steps, T_PSNR=T_PSNR, T_steps=T_steps,
                          T_PSNR_DIFF=T_PSNR_DIFF, config=config, verbose=verbose, device=device)

@@ -197,7 +197,7 @@ class Plan:
 
     @property
     def pipeline(self) -> int:
-        """hbx_plan_pipeline: _lib.PIPE_THREE_PASS / PIPE_COLBITS / PIPE_GENERIC."""
+        """hbx_plan_pipeline: _lib.PIPE_THREE_PASS (the only pipeline built since ABI v8)."""
         rc = int(self.lib.hbx_plan_pipeline(self._h))
         if rc < 0:
             _lib.check(rc, "hbx_plan_pipeline")
@@ -384,6 +384,14 @@ class Plan:
         n_ids = 0 if env_ids is None else int(env_ids.shape[0])
         _lib.check(self.lib.hbx_env_reset(self._h, C.byref(bufs), n_env, _ptr(env_ids), n_ids,
                                           _stream(stream)), "hbx_env_reset")
+
+    def env_obs_sync(self, bufs: _lib.EnvBuffers, n_env: int, what: int = _lib.OBS_STATE | _lib.OBS_RECON,
+                     env_ids: Optional[torch.Tensor] = None, stream=None):
+        """Rebuild the observation mirrors (state_bytes from the mask, recon from the
+        intensity cache) of the listed envs -- hbx_env_obs_sync."""
+        n_ids = 0 if env_ids is None else int(env_ids.shape[0])
+        _lib.check(self.lib.hbx_env_obs_sync(self._h, C.byref(bufs), n_env, _ptr(env_ids), n_ids, int(what),
+                                             _stream(stream)), "hbx_env_obs_sync")
 
     def env_step_psf(self, bufs, params, n_env, actions, reward, psnr, accepted, terminated, truncated,
                      stream=None):

@@ -31,12 +31,12 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 7
+#define HBX_ABI_VERSION 8
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
 #define HBX_ERR_HIP (-2)         /* HIP runtime error                             */
-#define HBX_ERR_UNSUPPORTED (-3) /* size not built (N must be 64, 256 or 1024)    */
+#define HBX_ERR_UNSUPPORTED (-3) /* size not built (N must be 64, 256, 896, 1024)  */
 #define HBX_ERR_NOMEM (-4)       /* workspace allocation failed                   */
 
 /* Transfer function (tt.simulate, env.py:172; SURVEY a4 assumptions as switches) */
@@ -62,7 +62,7 @@ extern "C" {
 /* Optics of one plan; replaces tt.Tensor meta {'dx','wl'} + simulate's z
  * (env.py:124,172; env_1024_24.py:135-138; DBS_1024_24.py:230-233). */
 typedef struct hbx_optics {
-  int32_t height;                        /* N (64, 256 or 1024), square      */
+  int32_t height;                        /* N (64, 256, 896 or 1024), square */
   int32_t width;                         /* == height                         */
   int32_t groups;                        /* G: 1 mono, 3 RGB                  */
   int32_t planes;                        /* P planes per group (even)         */
@@ -101,6 +101,26 @@ typedef struct hbx_env_buffers {
                                  env_group.py:198; nullable -> params value)  */
   int32_t imp_count;          /* 10000 in the reference                       */
   int32_t reserved;
+  /* ABI v8: zero-copy observations (env.py:135-140,176-181).  The reference
+   * hands out env.state itself as obs["state"] and the stepped reconstruction
+   * as obs["recon_image"]; these buffers are those observations, kept current
+   * by reset and step so a caller can alias them instead of rebuilding them. */
+  int8_t* state_bytes;     /* [B][G*P][H][W] 0/1 = the mask bits as int8:
+                              obs["state"] (nullable).  Written by hbx_env_reset
+                              / hbx_env_obs_sync and by the accepted flip of
+                              every step (both modes).                        */
+  float* recon;            /* [B][G][H][W] obs["recon_image"] (nullable; FFT
+                              mode only; needs intensity and recon_pending).
+                              After hbx_env_step the stepped group holds the
+                              stepped (pre-rollback) intensity, env.py:179,
+                              written there by the propagation itself; the
+                              other groups hold the cached accepted ones.     */
+  int32_t* recon_pending;  /* [B] internal: the group the next step reconciles
+                              between recon and intensity (+g+1: accepted,
+                              recon -> intensity; -(g+1): rolled back,
+                              intensity -> recon; 0: none).  With recon given,
+                              env->intensity of the last stepped group is
+                              current only after that reconcile.             */
 } hbx_env_buffers_t;
 
 /* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
@@ -121,7 +141,8 @@ int hbx_abi_version(void);
 const char* hbx_last_error(void);
 
 /* Plan: owns twiddles, transfer-function tables and a workspace for up to
- * `max_jobs` concurrent group propagations (64 MiB per job at N=1024).
+ * `max_jobs` concurrent group propagations (P * 12 * N^2 bytes per job:
+ * 96 MiB at N = 1024, P = 8; hbx_plan_workspace_bytes gives the total).
  * Replaces the per-call setup hidden inside tt.simulate (env.py:172). */
 int hbx_plan_create(hbx_plan_t* plan, const hbx_optics_t* optics, int32_t max_jobs,
                     int32_t device);
@@ -172,9 +193,13 @@ int hbx_env_reset(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
  * decode (env.py:157-161), flip + record, re-propagate the touched colour
  * group, relative PSNR, reward = RW * delta, rollback / bonus / termination.
  *   reward, psnr [B] f64; accepted, terminated, truncated [B] u8 (nullable)
- *   group_intensity [B][H][W] f32: the stepped (pre-rollback) group mean, the
- *   obs "recon_image" channel (nullable).  Accepted steps also refresh
- *   env->intensity[b][g] when that cache is non-null. */
+ *   group_intensity [B][H][W] f32: the stepped (pre-rollback) group mean
+ *   (nullable; not together with env->recon, which already holds it).
+ * With env->recon (ABI v8) the last pass writes the stepped intensity straight
+ * into recon[b][g] and the step starts by reconciling the previous step's
+ * group (one N^2 f32 copy per env); without it, accepted steps refresh
+ * env->intensity[b][g] when that cache is non-null.  env->state_bytes, when
+ * non-null, follows every accepted flip. */
 int hbx_env_step(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_env_params_t* params,
                  int32_t n_env, const int64_t* actions, double* reward, double* psnr,
                  uint8_t* accepted, uint8_t* terminated, uint8_t* truncated,
@@ -246,16 +271,18 @@ int hbx_commit_flip_psf(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_
  * serial loop's: every candidate before an accepted one was evaluated against
  * exactly the state the serial loop would have had.
  *
- * ABI v7: for K in {1, 2, 3, 4, 6, 8, 12, 16} a batch is ONE launch (k_walk_step):
+ * ABI v7: for K in 1..4 a batch is ONE launch (k_walk_step):
  * it first applies the previous batch's accepted flip(s) to field / intensity,
  * evaluates the K candidates on the updated state, and its last-arriving
  * workgroup decides; for K = 2..4 it also resolves the first candidate after
  * the first accept against the state WITH that accept (exact pairwise terms),
  * so a batch takes up to two accepts of the serial loop.  The accepted flips of
  * a batch therefore reach field / intensity in the NEXT launch: after the walk
- * is done make one more call (batches >= 1; it only commits).  Other K run the
+ * is done make one more call (batches >= 1; it only commits).  K > 4 runs the
  * three-launch batch of ABI v5 (eval / decide / commit; also selected for every
- * K by HBX_WALK_SPLIT=1 in the environment at plan creation).
+ * K by HBX_WALK_SPLIT=1 in the environment at plan creation); a call that
+ * switches from the one-launch to the three-launch form first issues one
+ * commit-only step for the pending accepts.
  *
  * The walk state lives in DEVICE memory (caller-owned; commit_ch = -1,
  * commit2_ch1 = 0, split_ch1 = 0 and the counters zero at the start); the caller reads it back
@@ -318,6 +345,17 @@ int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
 int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_env_params_t* params,
                      int32_t n_env, const int64_t* actions, double* reward, double* psnr,
                      uint8_t* accepted, uint8_t* terminated, uint8_t* truncated, void* stream);
+
+/* (ABI v8) Rebuild the observation mirrors of the listed envs (env_ids
+ * nullable = all n_env) from the state they mirror:
+ *   HBX_OBS_STATE  state_bytes <- the mask bits
+ *   HBX_OBS_RECON  recon <- intensity, recon_pending <- 0
+ * hbx_env_reset does both for the envs it resets; a caller that restores
+ * masks or intensities by itself (checkpoint load) calls it after. */
+#define HBX_OBS_STATE 1
+#define HBX_OBS_RECON 2
+int hbx_env_obs_sync(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
+                     const int32_t* env_ids, int32_t n_ids, int32_t what, void* stream);
 
 /* Exact re-propagation (FFT path) of env->field, env->intensity and
  * env->chan_stats for the listed envs (bounds the fp32 drift of the

@@ -48,6 +48,7 @@ int main(void) {
   CHECK(hbx_env_step(NULL, NULL, NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_env_step_psf(NULL, NULL, NULL, 0, NULL, NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_field_refresh(NULL, NULL, 0, NULL, 0, NULL) == HBX_ERR_INVALID);
+  CHECK(hbx_env_obs_sync(NULL, NULL, 0, NULL, 0, HBX_OBS_STATE, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_step(NULL, NULL, NULL, 0, NULL, NULL, NULL, NULL, NULL, 0, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_eval_flips(NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_eval_flips_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);

@@ -176,3 +176,53 @@ def test_gloo_world2_dbs_dataset_sharding(tmp_path):
     import numpy as np
     z = np.load(tmp_path / "r1" / "dbs_image3_accepted.npz")
     assert z["positions"].tolist() == [] and (tmp_path / "r0" / "dbs_image4_accepted.npz").exists()
+
+
+def _forced_world1_worker(out):
+    """hbx.dist.init(force=True) at world 1 without torchrun: a real (HashStore)
+    group, every collective through it, results equal to the world-less ones."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "binary-hologram-reinforcement-learning_amd")]
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        os.environ.pop(k, None)
+    from hbx import dbs
+    from hbx import dist as hd
+    from tests._probe_fake import OraclePlan, probe_inputs
+    B = 3
+    rows = hd.pack_step_metrics(torch.arange(B, dtype=torch.float64), torch.ones(B, dtype=torch.float64),
+                                torch.ones(B, dtype=torch.uint8), torch.zeros(B, dtype=torch.uint8),
+                                torch.zeros(B, dtype=torch.uint8))
+    ocfg, pre, tgt, mask, flips = probe_inputs()
+
+    def run():
+        mg = hd.StepMetricGather(B, every=2)
+        for k in range(3):
+            mg.add(rows[:, 0] + k, rows[:, 1], rows[:, 2], rows[:, 3], rows[:, 4])
+        mg.flush()
+        pr = dbs.probe_sharded(OraclePlan(ocfg), mask, tgt, flips, pre_model=pre)
+        return ([b.tolist() for b in mg.gathered], hd.gather_to_rank0(rows).tolist(), hd.max_over_ranks(2.5),
+                hd.describe_world(), pr.shard, pr.attempted_bins.tolist(), pr.improved_total)
+
+    plain = run()
+    assert not hd.active()
+    hd.init(backend="gloo", force=True)
+    assert hd.active() and hd.backend() == "gloo"
+    forced = run()
+    hd.barrier()
+    hd.shutdown()
+    out.put((plain, forced))
+
+
+@pytest.mark.timeout(120)
+def test_forced_world1_group_runs_every_collective():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_world1_worker, args=(q,))
+    p.start()
+    plain, forced = q.get(timeout=100)
+    p.join(timeout=30)
+    assert p.exitcode == 0
+    assert plain[3] == [[0, 1, 0, "none"]] and forced[3] == [[0, 1, 0, "gloo"]]
+    assert [len(b) for b in forced[0]] == [2, 1]
+    assert plain[:3] == forced[:3] and plain[4:] == forced[4:]

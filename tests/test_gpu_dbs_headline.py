@@ -85,6 +85,22 @@ def _first_difference(positions, accepted):
     return int(diff[0]) if len(diff) else None
 
 
+def _abs_psnr_resolution(plan, ocfg, tgt, n_states):
+    """Max |device PSNR - oracle PSNR| of one propagation over n_states seeded random
+    masks at the plan's size: the f32 resolution of an absolute PSNR."""
+    import hbx
+    prop = O.Propagator(ocfg)
+    worst = 0.0
+    for s in range(n_states):
+        m = (np.random.default_rng(1000 + s).random((ocfg.channels, ocfg.height, ocfg.width)) >= 0.5)
+        inten = prop.all_intensity(m.astype(np.uint8))
+        want = prop.psnr(np.stack([O.chan_stats(inten[g], tgt[g]) for g in range(ocfg.groups)]))
+        bits = hbx.pack_bits(torch.from_numpy(m).cuda())
+        _, _, ps = plan.propagate(bits[None], torch.from_numpy(tgt).cuda()[None], want_intensity=False)
+        worst = max(worst, abs(float(ps[0]) - want))
+    return worst
+
+
 def _gain_error(res, d, upto):
     acc_idx = np.nonzero(d["accepted"][:upto])[0]
     pos = np.asarray(res.accepted_positions, np.int64)
@@ -214,11 +230,21 @@ def test_dbs_ratio05_256_literal_run(golden_dir, mode):
         assert abs(float(d["delta"][first])) <= FFT_TOL_DB, (first, float(d["delta"][first]))
     if first is None:
         assert res.steps == n and res.stopped_early
-        # the final PSNR after 12,967 accepts (the walk re-propagates exactly every 4096): within
-        # the f32 resolution of an absolute 256x256 PSNR (measured 2.2e-8 walk, 3.8e-8 fft)
+        # Gain error bound, derived.  The gain is final - initial PSNR, each
+        # an ABSOLUTE PSNR of a state: the initial one from an f32 propagation, the final one
+        # (FFT mode) from the last accepted candidate's f32 re-propagation, or (walk) from the
+        # last exact f32 refresh plus the f64-summed increments of the accepts since.  So
+        #   |gain error| <= 2 E_abs  (+ accepts since the last refresh x INCR_TOL_DB, walk)
+        # with E_abs the f32 resolution of an absolute 256x256x8 PSNR, measured here on 16
+        # random states against the float64 oracle (max error x 1.5).
+        e_abs = 1.5 * _abs_psnr_resolution(plan, ocfg, tgt, 16)
+        n_acc = len(res.accepted_positions)
+        since = n_acc % 4096 if mode == "psf" else 0      # greedy's refresh_every default
+        bound = 2.0 * e_abs + since * INCR_TOL_DB
         gerr = abs((res.final_psnr - res.initial_psnr) - (float(d["final_psnr"]) - float(d["initial_psnr"])))
-        print(f"ratio05 {mode}: {res.steps} candidates, {len(res.accepted_positions)} accepts, gain error {gerr:.2e} dB")
-        assert gerr <= 2e-7
+        print(f"ratio05 {mode}: {res.steps} candidates, {n_acc} accepts, gain error {gerr:.2e} dB, "
+              f"E_abs {e_abs:.2e} dB, derived bound {bound:.2e} dB")
+        assert gerr <= bound
     assert abs(res.final_psnr - float(d["final_psnr"])) <= 1e-4
     plan.close()
 

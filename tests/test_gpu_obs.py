@@ -1,0 +1,138 @@
+"""Zero-copy observations (ABI v8, env.py:135-140,176-181).
+
+The reference hands out env.state itself as obs["state"] and the stepped
+reconstruction as obs["recon_image"].  HologramVecEnv now returns views of
+device buffers the reset / step kernels keep current (state_bytes, recon);
+these tests check the mirrors against what they mirror after many random
+steps with rollbacks:
+
+  obs["state"]        == unpack_bits(mask)                         bit-exact
+  obs["recon_image"]  stepped group == the propagated intensity of the stepped
+                      (pre-rollback) mask; other groups == the propagated
+                      intensity of the current mask                 bit-exact (same kernels)
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import hbx_oracle as O  # noqa: E402
+
+
+def _env(cfg, B, seed, **kw):
+    from hbx.env import HologramVecEnv
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    pres = [torch.rand((cfg.channels, cfg.height, cfg.width), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, cfg.height, cfg.width), generator=g, device="cuda") for _ in range(B)]
+    env = HologramVecEnv(cfg, B, lambda i: tgts[i], pre_model_source=lambda i: pres[i], auto_reset=False, **kw)
+    return env, g
+
+
+def _flip_words(mask, actions, cfg):
+    """mask (B, CH, H, W/64) with each env's action pixel toggled."""
+    m = mask.clone()
+    hw = cfg.height * cfg.width
+    for b, a in enumerate(actions.tolist()):
+        ch, pix = divmod(a, hw)
+        r, col = divmod(pix, cfg.width)
+        w = col // 64
+        bit = torch.tensor(1, dtype=torch.int64, device=m.device) << (col % 64)
+        m[b, ch, r, w] ^= bit
+    return m
+
+
+@pytest.mark.parametrize("N,steps", [(1024, 200), (256, 300)])
+def test_obs_mirrors_follow_steps_and_rollbacks(N, steps):
+    import hbx
+    from hbx.plan import unpack_bits
+    cfg = hbx.rgb_config(1024) if N == 1024 else hbx.mono_config(256)
+    B = 4
+    env, g = _env(cfg, B, 17 + N)
+    obs = env.reset()
+    st = env.state
+    assert obs["state"].data_ptr() == st.state_bytes.data_ptr()          # views, not copies
+    assert obs["recon_image"].data_ptr() == st.recon.data_ptr()
+    assert obs["state"].shape == (B, 1, cfg.channels, N, N) and obs["state"].dtype == torch.int8
+    assert torch.equal(st.state_bytes, unpack_bits(st.mask, N))
+    assert torch.equal(st.recon, st.intensity)
+    plan = hbx.Plan(cfg, max_jobs=B * cfg.groups)
+    acts = torch.randint(0, cfg.channels * N * N, (steps, B), generator=g, device="cuda")
+    n_acc = n_rej = 0
+    for k in range(steps):
+        pre_mask = st.mask.clone()
+        obs, r, dones, infos = env.step(acts[k])
+        assert obs["state"].data_ptr() == st.state_bytes.data_ptr()
+        assert torch.equal(st.state_bytes, unpack_bits(st.mask, N)), k
+        acc = env._acc.bool()
+        n_acc += int(acc.sum())
+        n_rej += int((~acc).sum())
+        if k % 20 == 0 or k == steps - 1:
+            stepped = _flip_words(pre_mask, acts[k], cfg)
+            tgt = st.target
+            i_step, _, _ = plan.propagate(stepped, tgt)
+            i_now, _, _ = plan.propagate(st.mask, tgt)
+            gidx = (acts[k] // (N * N)) // cfg.planes
+            for b in range(B):
+                for gg in range(cfg.groups):
+                    want = i_step[b, gg] if gg == int(gidx[b]) else i_now[b, gg]
+                    assert torch.equal(obs["recon_image"][b, 0, gg], want), (k, b, gg)
+    assert n_acc > 0 and n_rej > 0
+    # the accepted-state cache is current after the next step's reconcile; a reset re-syncs
+    env.reset_envs([1])
+    assert torch.equal(st.recon[1], st.intensity[1]) and int(st.recon_pending[1]) == 0
+    assert torch.equal(st.state_bytes, unpack_bits(st.mask, N))
+    plan.close()
+    env.close()
+
+
+def test_obs_state_mirror_incremental_mode():
+    """mode='psf' keeps obs["state"] in the same step kernel (k_env_step_finalize)."""
+    import hbx
+    from hbx.plan import unpack_bits
+    cfg = hbx.rgb_config(1024)
+    B = 3
+    env, g = _env(cfg, B, 5, mode="psf", refresh_every=64,
+                  obs_keys=("state_record", "state", "pre_model", "target_image"))
+    env.reset()
+    acts = torch.randint(0, cfg.channels * 1024 * 1024, (200, B), generator=g, device="cuda")
+    for k in range(200):
+        obs, _, _, _ = env.step(acts[k])
+    assert obs["state"].data_ptr() == env.state.state_bytes.data_ptr()
+    assert torch.equal(env.state.state_bytes, unpack_bits(env.state.mask, 1024))
+    assert 0 < int(env.state.flip_count.sum()) < 200 * B
+    env.close()
+
+
+def test_obs_step_matches_oracle_small():
+    """64 x 64 RGB: the observation dict after every step against the float64
+    oracle env (state exact, recon_image within 2e-5 * max, stepped group
+    pre-rollback), including rollbacks."""
+    import hbx
+    from hbx.env import HologramVecEnv
+    ocfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    pre, tgt = O.synthetic_inputs(ocfg, 21)
+    cfg = hbx.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    env = HologramVecEnv(cfg, 1, lambda i: tgt, pre_model_source=lambda i: pre, auto_reset=False)
+    env.reset()
+    ref = O.OracleEnv(ocfg)
+    ref.reset(pre, tgt)
+    prop = O.Propagator(ocfg)
+    rng = np.random.default_rng(4)
+    saw = set()
+    for a in rng.integers(0, ocfg.channels * 64 * 64, 40):
+        obs, _, _, _ = env.step(torch.tensor([int(a)], device="cuda"))
+        before = ref.state.copy()
+        res = ref.step(int(a))
+        saw.add(res.accepted)
+        c, r, col = O.decode_action(int(a), 64, 64)
+        stepped = before.copy()
+        stepped[c, r, col] ^= 1
+        want_rec = prop.all_intensity(ref.state)
+        gs = c // ocfg.planes
+        want_rec[gs] = prop.group_intensity(stepped, gs)
+        got = obs["recon_image"][0, 0].cpu().numpy()
+        assert np.max(np.abs(got - want_rec)) <= 2e-5 * np.max(want_rec)
+        assert np.array_equal(obs["state"][0, 0].cpu().numpy(), ref.state.astype(np.int8))
+    assert saw == {True, False}
+    env.close()

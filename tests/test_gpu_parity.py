@@ -163,74 +163,6 @@ def test_eval_flips_1024_vs_oracle():
     assert np.max(np.abs(got.cpu().numpy() - np.array(want))) <= PSNR_TOL
 
 
-def _plan_path(cfg, max_jobs, legacy):
-    """Plan on the three-pass path (default) or the bits -> column path (HBX_COLBITS=1)."""
-    import hbx
-    old = os.environ.pop("HBX_COLBITS", None)
-    try:
-        if not legacy:
-            os.environ["HBX_COLBITS"] = "1"
-        plan = hbx.Plan(cfg, max_jobs=max_jobs)
-        assert plan.pipeline == (hbx._lib.PIPE_THREE_PASS if legacy else hbx._lib.PIPE_COLBITS)
-        return plan
-    finally:
-        os.environ.pop("HBX_COLBITS", None)
-        if old is not None:
-            os.environ["HBX_COLBITS"] = old
-
-
-@pytest.mark.parametrize("field_kind", [0, 1])   # amplitude {0,1}, binary phase {+1,-1}
-def test_colbits_matches_three_pass_1024(field_kind):
-    """N = 1024: the bits -> column pass (hbx_colbits.hip) against the three-pass
-    path on 8 envs (24 jobs: the XCD job mapping) with flips on every row class:
-    stats rtol 2e-6, intensity 2e-6 * max; and the legacy path itself vs the oracle."""
-    import hbx
-    cfg = hbx.rgb_config(1024, field_kind=field_kind)
-    g = torch.Generator(device="cuda").manual_seed(11)
-    pre = torch.rand((8, 24, 1024, 1024), generator=g, device="cuda")
-    bits = hbx.pack_bits(pre >= 0.5)
-    tgt = torch.rand((8, 3, 1024, 1024), generator=g, device="cuda")
-    new = _plan_path(cfg, 24, legacy=False)
-    old = _plan_path(cfg, 24, legacy=True)
-    a = new.propagate(bits, tgt)
-    b = old.propagate(bits, tgt)
-    torch.cuda.synchronize()
-    assert torch.allclose(a[1], b[1], rtol=2e-6, atol=0)
-    assert float((a[0] - b[0]).abs().max()) <= 2e-6 * float(b[0].abs().max())
-    assert float((a[2] - b[2]).abs().max()) <= 1e-5
-    # flips: every colour plane, rows / columns at the class boundaries (x mod 64 = 0, 31, 32, 63)
-    n = 1024 * 1024
-    fl = [c * n + r * 1024 + x for c in (0, 5, 8, 15, 16, 23) for (r, x) in
-          ((0, 0), (1023, 1023), (511, 31), (512, 32), (7, 63), (300, 64 * 7 + 33))]
-    flips = torch.tensor(fl, dtype=torch.int64, device="cuda")
-    st0 = a[1][0].contiguous()
-    pa, _ = new.eval_flips(bits[0], tgt[0], st0, flips)
-    pb, _ = old.eval_flips(bits[0], tgt[0], st0, flips)
-    torch.cuda.synchronize()
-    assert float((pa - pb).abs().max()) <= 2e-5
-
-
-def test_colbits_1024_vs_oracle_flips():
-    """The bits -> column path against the float64 oracle: full propagation and 8 flips
-    (K = 8 jobs, XCD mapping), amplitude field."""
-    import hbx
-    ocfg = O.rgb_config(1024)
-    pre, tgt = O.synthetic_inputs(ocfg, 4)
-    env = O.OracleEnv(ocfg)
-    env.reset(pre, tgt)
-    n = 1024 * 1024
-    flips = np.array([0, n - 1, 3 * n + 64 * 5, 9 * n + 5 * 1024 + 77, 12 * n + 1023 * 1024 + 32,
-                      17 * n + 512 * 1024 + 511, 20 * n + 33, 24 * n - 1], np.int64)
-    want = [env.evaluate_flip(int(f))[0] for f in flips]
-    plan = _plan_path(dev_cfg(ocfg), 8, legacy=False)
-    bits = to_dev_bits(O.pack_mask((pre >= 0.5).astype(np.uint8)))
-    _, st, ps = plan.propagate(bits[None], torch.from_numpy(tgt).cuda()[None])
-    assert abs(float(ps[0]) - env.initial_psnr) <= PSNR_TOL
-    got, _ = plan.eval_flips(bits, torch.from_numpy(tgt).cuda(), st[0].contiguous(),
-                             torch.from_numpy(flips).cuda())
-    assert np.max(np.abs(got.cpu().numpy() - np.array(want))) <= PSNR_TOL
-
-
 # -- env semantics ---------------------------------------------------------------------------
 def test_env_trace_golden(golden_dir):
     import hbx
@@ -712,6 +644,55 @@ def test_dbs_greedy_incremental_mode(golden_dir, refresh, mode):
     assert np.array_equal(mask.cpu().numpy().view("<u8"), d["final_mask_bits"])
 
 
+@pytest.mark.parametrize("refresh", [4096, 7])
+def test_walk_repeated_positions_fused_split_host_oracle(monkeypatch, refresh):
+    """Orders that revisit pixels: consecutive repeats, a period-3 cycle
+    over three pixels and revisits one candidate apart, so a batch holds a candidate on
+    the first accept's pixel (the fused step breaks there and re-evaluates it in the next
+    launch) and pending commits sit on a candidate's pixel (the WalkPre sign toggle).
+    K cycles through the fused depths 2, 3, 4 every chunk.  The fused walk, the split
+    three-launch walk (HBX_WALK_SPLIT=1) and the host-decided batches accept exactly the
+    same positions, and all of them the serial float64 oracle's wherever its change is
+    resolved (|change| > 1e-7 dB)."""
+    import hbx
+    from hbx import dbs
+    ocfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB)
+    pre, tgt = O.synthetic_inputs(ocfg, 33)
+    cfg = dev_cfg(ocfg)
+    n_pix = ocfg.channels * 64 * 64
+    base = np.random.default_rng(9).integers(0, n_pix, 400)
+    i = np.arange(600)
+    order = np.concatenate([base[i // 3 + (i % 3 == 2)],           # b0 b0 b1 b1 b1 b2 ...
+                            base[400 - 3:][i % 3],                   # a b c a b c ...
+                            base[(i // 2) + (i % 2) * 2]])           # b0 b2 b1 b3 b2 b4 ...
+    ks = [2, 3, 4]
+    it = iter(range(10 ** 6))
+    monkeypatch.setattr(dbs, "walk_k", lambda *a, **k: ks[next(it) % len(ks)])
+    env = O.OracleEnv(ocfg)
+    env.reset(pre, tgt)
+    want, psnrs, _ = O.dbs_greedy(env, order)
+    prev = np.maximum.accumulate(np.concatenate([[env.initial_psnr], psnrs]))[:-1]
+    clear = np.abs(psnrs - prev) > 1e-7
+    runs = {}
+    for name in ("psf", "split", "psf_host"):
+        if name == "split":
+            monkeypatch.setenv("HBX_WALK_SPLIT", "1")
+        plan = hbx.Plan(cfg, max_jobs=16)
+        monkeypatch.delenv("HBX_WALK_SPLIT", raising=False)
+        mask = hbx.pack_bits(torch.from_numpy(pre).cuda() >= 0.5)
+        res = dbs.greedy(plan, mask, torch.from_numpy(tgt).cuda(), order,
+                         mode="psf_host" if name == "psf_host" else "psf", refresh_every=refresh)
+        plan.close()
+        got = np.zeros(len(order), bool)
+        got[res.accepted_positions] = True
+        runs[name] = (got, mask.cpu().numpy())
+        assert res.steps == len(order)
+        assert np.array_equal(got[clear], want[clear]), (name, int(np.nonzero(got[clear] != want[clear])[0][0]))
+    assert np.array_equal(runs["psf"][0], runs["split"][0]) and np.array_equal(runs["psf"][1], runs["split"][1])
+    assert np.array_equal(runs["psf"][0], runs["psf_host"][0])
+    assert 0 < want.sum() < len(order) and (~clear).sum() < 5
+
+
 def test_dbs_walk_early_stop_and_prefix():
     """Device walk: DBS_ratio_0.5.py's early stop (stop_diff) against the serial
     oracle, and a max_candidates prefix ends exactly at the prefix."""
@@ -853,53 +834,34 @@ def _crop_inputs(seed):
     return ocfg, pre_c, tgt_c, bits
 
 
-def _plan_896(cfg, max_jobs, generic):
-    """Plan on the fused 896 path (default) or the composed one (HBX_GENERIC896=1)."""
+@pytest.mark.parametrize("field_kind", [O.FIELD_AMPLITUDE, O.FIELD_PHASE])
+def test_crop_896_lane_class_edges_vs_oracle(field_kind):
+    """N = 896 (the fused mixed-radix passes, hbx_passes896.hip) against the float64
+    oracle at the row / column edges of every slot lane class (x, y = 27 / 28 / 447 /
+    448 / 895 ...): the plane field of hbx_simulate (2e-6 * max), the propagated
+    statistics, and flips there (1e-4 dB).  Round 2 checked the fused path against a
+    composed one; that path is gone and the oracle pins 896 directly."""
     import hbx
-    old = os.environ.pop("HBX_GENERIC896", None)
-    try:
-        if generic:
-            os.environ["HBX_GENERIC896"] = "1"
-        plan = hbx.Plan(cfg, max_jobs=max_jobs)
-        assert plan.pipeline == (hbx._lib.PIPE_GENERIC if generic else hbx._lib.PIPE_THREE_PASS)
-        return plan
-    finally:
-        os.environ.pop("HBX_GENERIC896", None)
-        if old is not None:
-            os.environ["HBX_GENERIC896"] = old
-
-
-@pytest.mark.parametrize("field_kind", [0, 1])
-def test_crop_896_fused_matches_composed(field_kind):
-    """N = 896: the fused three-pass path (hbx_passes896.hip) against the composed
-    mixed-radix path on 6 envs (18 jobs), flips at the row / column edges of
-    every slot lane class: stats rtol 2e-6, intensity and field 2e-6 * max."""
-    import hbx
-    cfg = hbx.rgb_config(896, field_kind=field_kind)
-    g = torch.Generator(device="cuda").manual_seed(12)
-    pre = torch.rand((6, 24, 896, 896), generator=g, device="cuda")
-    bits = hbx.pack_bits(pre >= 0.5)
-    tgt = torch.rand((6, 3, 896, 896), generator=g, device="cuda")
-    new = _plan_896(cfg, 18, generic=False)
-    old = _plan_896(cfg, 18, generic=True)
-    a = new.propagate(bits, tgt)
-    b = old.propagate(bits, tgt)
-    torch.cuda.synchronize()
-    assert torch.allclose(a[1], b[1], rtol=2e-6, atol=0)
-    assert float((a[0] - b[0]).abs().max()) <= 2e-6 * float(b[0].abs().max())
-    assert float((a[2] - b[2]).abs().max()) <= 1e-5
-    fa, _ = new.simulate(bits[:1])
-    fb, _ = old.simulate(bits[:1])
-    assert float((fa - fb).abs().max()) <= 2e-6 * float(fb.abs().max())
+    _, pre, tgt, bits = _crop_inputs(12)
+    ocfg = O.rgb_config(896, field_kind=field_kind)
+    mask = (pre >= 0.5).astype(np.uint8)
+    plan = hbx.Plan(dev_cfg(ocfg), max_jobs=12)
+    t = torch.from_numpy(tgt).cuda()
+    fld, _ = plan.simulate(bits[None])
+    want_f = O.propagate(O.mask_to_field(mask[:2], field_kind), ocfg.transfer(0))
+    got_f = fld[0, :2].cpu().numpy()
+    assert np.max(np.abs(got_f - want_f)) <= 2e-6 * np.max(np.abs(want_f))
+    env = O.OracleEnv(ocfg)
+    base = env.reset(pre, tgt)
+    _, st, p0 = plan.propagate(bits[None], t[None])
+    assert abs(float(p0[0]) - base) <= PSNR_TOL
     n = 896 * 896
-    fl = [c * n + r * 896 + x for c in (0, 7, 8, 16, 23) for (r, x) in
-          ((0, 0), (895, 895), (447, 27), (448, 28), (5, 447), (300, 448), (1, 895 - 31))]
-    flips = torch.tensor(fl, dtype=torch.int64, device="cuda")
-    st0 = a[1][0].contiguous()
-    pa, _ = new.eval_flips(bits[0], tgt[0], st0, flips)
-    pb, _ = old.eval_flips(bits[0], tgt[0], st0, flips)
-    torch.cuda.synchronize()
-    assert float((pa - pb).abs().max()) <= 2e-5
+    fl = np.array([c * n + r * 896 + x for c in (0, 7, 16, 23) for (r, x) in
+                   ((0, 0), (895, 895), (447, 27), (448, 28), (300, 448), (1, 895 - 31))], np.int64)
+    want = np.array([env.evaluate_flip(int(a))[0] for a in fl])
+    got, _ = plan.eval_flips(bits, t, st[0].contiguous(), torch.from_numpy(fl).cuda())
+    assert np.max(np.abs(got.cpu().numpy() - want)) <= PSNR_TOL
+    plan.close()
 
 
 def test_crop_896_propagate_vs_oracle():
