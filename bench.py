@@ -440,6 +440,12 @@ def rounded(passes):
 
 def main():
     args = parse()
+    # the driver reads ONE JSON line from stdout: keep a handle on the real stdout and point
+    # fd 1 at stderr, so library banners (RCCL prints its version block on stdout when the
+    # communicator is created) cannot land on it
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     import torch
     from hbx import dist as hd
     from hbx.env import HologramVecEnv
@@ -659,7 +665,7 @@ def main():
                     out["cpu_baseline_scipy"] = cpu_baseline_scipy(max(4, args.cpu_sample), N, workers)
                 except Exception as e:  # scipy is optional on the box
                     out["cpu_baseline_scipy"] = {"error": str(e)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     hd.shutdown()
 
 

@@ -220,6 +220,9 @@ __device__ __forceinline__ float2 twiddle_const(float2 d, int k, int M) {
 
 template <int R, bool INV>
 __device__ __forceinline__ void dft_reg_scalar(float2 (&v)[R]) {
+#ifdef HBX_EXP_NODFT
+  return;
+#endif
 #pragma unroll
   for (int span = R / 2; span >= 1; span >>= 1) {
 #pragma unroll
@@ -291,6 +294,42 @@ __device__ __forceinline__ pk2 ld_pk(const T& a) {
 template <class T>
 __device__ __forceinline__ T st_pk(pk2 a) {
   if constexpr (std::is_same<T, pk2>::value) return a; else return from_pk(a);
+}
+
+// fft_group in two halves: s1 = the first DFT over j and the twiddles (registers and the
+// LDS twiddle table only), s2 = the transpose through the group's scratch and the second
+// DFT.  A kernel that shares the scratch with other work can sit a barrier between them.
+template <int R, bool INV, bool SCALAR = false, class T>
+__device__ __forceinline__ void fft_group_s1(T (&v)[R], int t, const float2* tw) {
+  asm volatile("" ::: "memory");
+  if constexpr (SCALAR) {
+    static_assert(std::is_same<T, float2>::value, "scalar FFT works on float2");
+    dft_reg_scalar<R, INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) {
+      const float2 w = tw[k1 * R + t];
+      v[k1] = INV ? cmulc(v[k1], w) : cmul(v[k1], w);
+    }
+  } else {
+    dft_reg<R, INV>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) {
+      const pk2 w = to_pk(tw[k1 * R + t]);
+      v[k1] = st_pk<T>(INV ? pk_cmulc(ld_pk(v[k1]), w) : pk_cmul(ld_pk(v[k1]), w));
+    }
+  }
+}
+template <int R, bool INV, bool SCALAR = false, class Scratch, class T>
+__device__ __forceinline__ void fft_group_s2(T (&v)[R], int t, const Scratch& sc) {
+  wave_sync();  // previous users of the scratch are done
+#pragma unroll
+  for (int k1 = 0; k1 < R; ++k1) *reinterpret_cast<T*>(sc.at(t, k1)) = v[k1];
+  wave_sync();
+#pragma unroll
+  for (int tt = 0; tt < R; ++tt) v[tt] = *reinterpret_cast<const T*>(sc.at(tt, t));
+  wave_sync();
+  if constexpr (SCALAR) dft_reg_scalar<R, INV>(v);
+  else dft_reg<R, INV>(v);
 }
 
 template <int R, bool INV, bool SCALAR = false, class Scratch, class T>

@@ -76,6 +76,22 @@ using LayoutA = PanelLine<R, R * R / 2, pan_a(R)>;
 template <int R>
 using LayoutB = PanelLine<R, R * R, pan_b(R)>;
 
+// B at N = 1024 (r03): 1-KB tiles [y / 16][s / 8][16 rows][8 slots] of the line SLOT
+//   s(kx) = kx (kx <= N/2),  3N/2 - kx (kx > N/2),
+// so the two output line sets of a k_col2 block -- lines kx0..kx0+7 and their mirrors
+// N - kx0 - 7 .. N - kx0 (N/2 for kx = 0) -- each fill one aligned tile, which the block
+// writes as one contiguous KB per 16-row band (staged through LDS), and a k_rowinv block
+// (8 rows) reads 512-B runs.  Replayed without arithmetic (tools/membw3.hip): k_col2's
+// movement 2.43 ms (today's 16-row panels 2.47), k_rowinv's 1.37 ms (1.62): DESIGN.md 4.
+struct TileB32 {
+  static constexpr int N = 1024;
+  __device__ static constexpr int line(int s) { return s <= N / 2 ? s : 3 * N / 2 - s; }
+  __device__ static constexpr int at(int s, int y) {   // float2 offset of (slot s, row y)
+    return (((y >> 4) * (N / 8) + (s >> 3)) << 7) + ((y & 15) << 3) + (s & 7);
+  }
+};
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
@@ -345,6 +361,39 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
 
+// N = 1024: the output line sets of a k_col2 block (8 lines: group g = slot g of slot
+// tile st, TileB32) go out through the FFT scratch.  col2_stage_write: each group
+// writes its line (imaginary part times sy) into its OWN scratch region (the group's
+// FFT is done with it; no block barrier), [band 64][row 16] at offset 4 g (a bank
+// shift that makes the readers' b64 loads conflict-free).  After a block barrier,
+// col2_stage_store: the block stores the set as 16-B chunks (slots 2 sp, 2 sp + 1 from
+// regions 2 sp, 2 sp + 1) in memory order -- one contiguous KB per 16-row band.
+__device__ __forceinline__ float2* col2_region(float2* scratch, int g) { return scratch + g * (32 * 33) + 4 * g; }
+
+__device__ __forceinline__ void col2_stage_write(const float2 (&v)[32], float sy, float2* scratch, int grp, int t) {
+  float2* reg = col2_region(scratch, grp);
+#pragma unroll
+  for (int k2 = 0; k2 < 32; ++k2) reg[32 * k2 + t] = make_float2(v[k2].x, sy * v[k2].y);   // (band, row) = y
+}
+
+template <int SK>
+__device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
+  // chunk c = tid + 256 i: band c / 64 = tid / 64 + 4 i, row (c / 4) % 16 = (tid / 4) % 16, slot pair
+  // c % 4 = tid % 4; memory offset = lane part + (st * 128 + i * 65536) float2 (the latter in soffset)
+  const int tid = threadIdx.x, sp = tid & 3;
+  const int y0 = ((tid >> 6) << 4) + ((tid >> 2) & 15);
+  const float2* lo_r = col2_region(const_cast<float2*>(scratch), 2 * sp) + y0;
+  const float2* hi_r = col2_region(const_cast<float2*>(scratch), 2 * sp + 1) + y0;
+  const int voff = (((tid >> 6) << 14) + (((tid >> 2) & 15) << 3) + 2 * sp) * 8;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float2 lo = store_round<SK>(lo_r[64 * i]);
+    const float2 hi = store_round<SK>(hi_r[64 * i]);
+    const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
+    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 128 + i * 65536) * 8, 0);
+  }
+}
+
 template <int R, int SK>
 __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
                                                  const float2* __restrict__ ws_a,
@@ -396,7 +445,13 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * N + t) * 8;
-    fft_group<R, false, true>(v, t, sc, tw);
+    if constexpr (R == 32) {
+      fft_group_s1<R, false, true>(v, t, tw);
+      if (it > 0) lds_barrier();   // the previous iteration's second set has been read out
+      fft_group_s2<R, false, true>(v, t, sc);
+    } else {
+      fft_group<R, false, true>(v, t, sc, tw);
+    }
     float2 w[R];
     if (!dc) {   // v <- Z H, w <- Z conj H, each H value consumed as it arrives
 #pragma unroll
@@ -422,23 +477,41 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       }
     }
     fft_group<R, true, true>(v, t, sc, tw);
-    {
-      const int vo = PB::voff(t, kx);
+    const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
+    if constexpr (R == 32) {
+      const int kxb = kx - grp;            // the block's 8 lines: slot tile kxb / 8
+      col2_stage_write(v, 1.0f, scratch, grp, t);
+      lds_barrier();
+      col2_stage_store<SK>(scratch, rb, kxb >> 3);
+      if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
+        const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(v[k2]), rb, vo, PB::joff(k2));
-    }
-    if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
-      const int vo = PA::voff(t, kx + KSTEP);
+        for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
+      }
+      fft_group_s1<R, true, true>(w, t, tw);
+      lds_barrier();   // the first set has been read out: the regions are the FFTs' again
+      fft_group_s2<R, true, true>(w, t, sc);
+      col2_stage_write(w, sy, scratch, grp, t);
+      lds_barrier();
+      col2_stage_store<SK>(scratch, rb, (N / 2 + kxb) >> 3);
+    } else {
+      {
+        const int vo = PB::voff(t, kx);
 #pragma unroll
-      for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
-    }
-    fft_group<R, true, true>(w, t, sc, tw);
-    {
-      const int vo = PB::voff(t, dc ? N / 2 : N - kx);
-      const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
+        for (int k2 = 0; k2 < R; ++k2) buf_st2s(store_round<SK>(v[k2]), rb, vo, PB::joff(k2));
+      }
+      if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
+        const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
-      for (int k2 = 0; k2 < R; ++k2)
-        buf_st2s(store_round<SK>(make_float2(w[k2].x, sy * w[k2].y)), rb, vo, PB::joff(k2));
+        for (int jj = 0; jj < R; ++jj) v[jj] = buf_ld2s(ra, vo, PA::joff(jj));
+      }
+      fft_group<R, true, true>(w, t, sc, tw);
+      {
+        const int vo = PB::voff(t, dc ? N / 2 : N - kx);
+#pragma unroll
+        for (int k2 = 0; k2 < R; ++k2)
+          buf_st2s(store_round<SK>(make_float2(w[k2].x, sy * w[k2].y)), rb, vo, PB::joff(k2));
+      }
     }
   }
 }
@@ -490,6 +563,85 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
     double* o = partial + ((size_t)j * RB + rb) * 3;
     o[0] = a; o[1] = b; o[2] = cc;
   }
+}
+
+// k_rowinv at N = 1024 (r03): every lane loads its own FFT input straight from the
+// tiled B (TileB32) -- lane t of group g (row y0 + g) needs kx = t + 32 jj, which for
+// 8 consecutive lanes is 8 consecutive slots of one tile row (64 B; the two rows of a wave
+// are adjacent: 128 B), so no LDS tile and no block barrier sit in the plane loop: the
+// group's FFT transpose (wave_sync) is its only LDS traffic.  Two register sets
+// alternate by plane, the next plane's loads in flight under this plane's FFT.  The
+// r02 kernel staged each plane through a 64-KB LDS tile between three block barriers.
+__global__ __launch_bounds__(256, 2) void k_rowinv32(const JobDesc* __restrict__ jobs,
+                                                     const float2* __restrict__ ws_b,
+                                                     const float* __restrict__ target,
+                                                     const float2* __restrict__ tw_glob, int P, int G,
+                                                     double* __restrict__ partial, float* __restrict__ inten_out,
+                                                     float2* __restrict__ field_out, size_t tmask, int inten_by_env) {
+  constexpr int R = 32, N = 1024, GPB = 8, RB = N / GPB;
+  __shared__ float2 tw[N];
+  __shared__ float2 scratch[GPB * R * (R + 1)];
+  __shared__ double red[GPB][3];
+  for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
+
+  const int grp = threadIdx.x / R;
+  const int t = threadIdx.x % R;
+  const int bid = xcd_pair<RB>(blockIdx.x);
+  const int rb = bid % RB;
+  const int j = bid / RB;
+  const JobDesc jb = jobs[j];
+  if (jb.env < 0) {
+    if (threadIdx.x == 0) {
+      double* o = partial + ((size_t)j * RB + rb) * 3;
+      o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
+    }
+    return;
+  }
+  const int y = rb * GPB + grp;
+  constexpr int PLB = N * N;                 // float2 per B plane
+  const __amdgpu_buffer_rsrc_t rs = plane_rsrc(ws_b + (size_t)j * P * PLB, (unsigned)((size_t)P * PLB * 8));
+  // lane bases (bytes) of this row: slot s of row y at TileB32::at(s, y).
+  //   jj < 16 (and kx = 512 for t = 0): s = kx = t + 32 jj -> lo + 4096 jj
+  //   jj >= 16 otherwise: s = 3N/2 - kx = 1536 - t - 32 jj -> hi - 4096 jj, written as
+  //   hi31 + 4096 (31 - jj) so every offset stays non-negative
+  const int yb = ((y >> 4) << 14) + ((y & 15) << 3);
+  const int m = t >> 3, u = t & 7;
+  const int lo = (yb + (m << 7) + u) * 8;
+  const int hi31 = (yb + (u ? ((191 - m) << 7) + 8 - u : (192 - m) << 7) - 512 * 31) * 8;
+  const int v16 = t == 0 ? lo + 4096 * 16 : hi31 + 4096 * 15;
+  auto load_plane = [&](pk2 (&v)[R], int p) {
+    const int po = p * PLB * 8;
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const int vo = jj < 16 ? lo : (jj == 16 ? v16 : hi31);
+      const int so = po + (jj < 16 ? 4096 * jj : (jj == 16 ? 0 : 4096 * (31 - jj)));
+      v[jj] = to_pk(buf_ld2s(rs, vo, so));
+    }
+  };
+  float acc[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) acc[k] = 0.0f;
+  const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+  auto finish_plane = [&](pk2 (&v)[R], int p) {
+    fft_group<R, true>(v, t, sc, tw);
+#pragma unroll
+    for (int k = 0; k < R; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+    if (field_out) {  // exact field of this plane (incremental mode init / refresh)
+      float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * N + y) * N;
+#pragma unroll
+      for (int k = 0; k < R; ++k) frow[t + R * k] = from_pk(v[k]);
+    }
+  };
+  pk2 va[R];
+  load_plane(va, 0);
+  __syncthreads();  // tw visible
+#pragma unroll 1
+  for (int p = 0; p < P; ++p) {              // the next plane's loads issued as soon as this one's FFT is done
+    finish_plane(va, p);
+    load_plane(va, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
+  }
+
+  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
 }
 
 template <int R, int NT>
@@ -746,9 +898,14 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
-    hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
-                       target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
-                       field_out, target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
+    if constexpr (R == 32)
+      hipLaunchKernelGGL(k_rowinv32, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
+                         pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
+                         pd.inten_by_env);
+    else
+      hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
+                         target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
+                         field_out, target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
     if (tm) tm->end(2, n_jobs, st);
   }
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial,
