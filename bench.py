@@ -62,8 +62,11 @@ def parse():
                     help="skip the SB3-facing step with all five observations (vecenv_step_obs)")
     ap.add_argument("--no-precision", action="store_true",
                     help="skip the fp32-vs-bf16 intermediate-storage deviation (SURVEY 8d cfg 5)")
-    ap.add_argument("--gather-every", type=int, default=1,
-                    help="world > 1: steps of per-env metrics per gather to rank 0 (hbx.dist.StepMetricGather)")
+    ap.add_argument("--gather-every", type=int, default=8,
+                    help="steps of per-env metrics per gather to rank 0 (hbx.dist.StepMetricGather; "
+                         "the step kernel writes into the gather rows, one dist.gather per K steps)")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="pass-timing hipEvent pairs on every K-th launch of each pass in the timed loop")
     return ap.parse_args()
 
 
@@ -477,7 +480,7 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i))
         return torch.rand((CH, N, N), generator=g, device="cuda")
 
-    def measure(mode: str, steps: int, warmup: int, mcfg=None):
+    def measure(mode: str, steps: int, warmup: int, mcfg=None, timing_every=None):
         mcfg = mcfg or cfg
         mG, mCH, mN = mcfg.groups, mcfg.channels, mcfg.height
 
@@ -497,16 +500,18 @@ def main():
         mg = hd.StepMetricGather(B, args.gather_every, dev) if gather else None
 
         def one_step(k):
-            r, ps, acc, term, trunc = vec.step_device(actions[k])
             if mg is not None:
-                mg.add(r, ps, acc, term, trunc)
+                mg.add(*vec.step_device(actions[k], out=mg.slot()))
+            else:
+                vec.step_device(actions[k])
 
         for k in range(warmup):
             one_step(k)
         if mg is not None:
             mg.flush()
         torch.cuda.synchronize()
-        vec.plan.set_timing(steps * -(-B // (args.chunk or B)) + 1)
+        vec.plan.set_timing(steps * -(-B // (args.chunk or B)) + 1,
+                            timing_every or args.timing_every)
         hd.barrier()
         torch.cuda.synchronize()
         acc0 = int(vec.state.flip_count.sum().item())
@@ -543,7 +548,9 @@ def main():
                 traffic = kinfo.get("hbm_bytes_per_launch")
         roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4)}
+                    "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4),
+                    "timing": f"hipEvent pairs on the launch stream around every {args.timing_every}-th launch "
+                              f"of each pass inside the timed loop ({d['launches']} launches of {dom})"}
         step_bytes = sum(abytes[k] for k in timing if k in ("k_rowfwd", "k_col", "k_rowinv")) * B
         canon = canonical_step_bytes(N, P)
         out = {
@@ -609,7 +616,8 @@ def main():
         torch.cuda.empty_cache()
 
     if not args.no_psf:
-        vec, dt, timing, acc_rate = measure("psf", args.psf_steps, max(args.warmup, 5))
+        vec, dt, timing, acc_rate = measure("psf", args.psf_steps, max(args.warmup, 5),
+                                          timing_every=1)   # k_psf_commit is charged the timed accepts
         if rank == 0:
             ps = pass_table(timing, abytes, {"k_psf_commit": vec.timed_accepts})
             ev = ps.get("k_psf_eval")

@@ -864,10 +864,13 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
 
 extern "C" {
 
-int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
+int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) { return hbx_plan_set_timing_sampled(p, capacity, 1); }
+
+int hbx_plan_set_timing_sampled(hbx_plan_t p, int32_t capacity, int32_t every) {
   int rc = check_plan(p);
   if (rc) return rc;
   if (capacity < 0) return fail(HBX_ERR_INVALID, "capacity");
+  if (every < 1) return fail(HBX_ERR_INVALID, "every");
   (void)hipSetDevice(p->device);
   hbx::PassTimer* tm = p->pd.timer;
   if (tm) {
@@ -892,6 +895,7 @@ int hbx_plan_set_timing(hbx_plan_t p, int32_t capacity) {
     delete tm;
   };
   tm->capacity = capacity;
+  tm->every = every;
   for (int k = 0; k < hbx::kNumPasses; ++k) {
     tm->ev[k] = new (std::nothrow) hipEvent_t[2 * (size_t)capacity];
     if (!tm->ev[k]) {
@@ -934,6 +938,7 @@ int hbx_plan_read_timing(hbx_plan_t p, double* ms_total, int64_t* launches, int6
     launches[k] = tm->count[k];
     if (jobs) jobs[k] = tm->jobs[k];
     tm->count[k] = 0;
+    tm->calls[k] = 0;
     tm->jobs[k] = 0;
   }
   return HBX_OK;

@@ -220,9 +220,6 @@ __device__ __forceinline__ float2 twiddle_const(float2 d, int k, int M) {
 
 template <int R, bool INV>
 __device__ __forceinline__ void dft_reg_scalar(float2 (&v)[R]) {
-#ifdef HBX_EXP_NODFT
-  return;
-#endif
 #pragma unroll
   for (int span = R / 2; span >= 1; span >>= 1) {
 #pragma unroll

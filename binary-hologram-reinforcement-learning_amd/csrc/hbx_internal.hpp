@@ -88,21 +88,27 @@ struct PanelLine {
   }
 };
 
-// Optional hipEvent pairs around every pass launch (hbx_plan_set_timing).
+// Optional hipEvent pairs around every `every`-th pass launch (hbx_plan_set_timing*).
 constexpr int kNumPasses = 5;  // rowfwd, col, rowinv, psf_eval, psf_commit
 struct PassTimer {
   int capacity = 0;
+  int every = 1;
   int count[kNumPasses] = {};
+  int64_t calls[kNumPasses] = {};   // launches seen (recorded or not)
+  bool open[kNumPasses] = {};       // begin() recorded, end() pending
   int64_t jobs[kNumPasses] = {};
   hipEvent_t* ev[kNumPasses] = {};  // [2 * capacity] start/stop
   __host__ void begin(int pass, hipStream_t st) {
-    if (capacity && count[pass] < capacity) (void)hipEventRecord(ev[pass][2 * count[pass]], st);
+    open[pass] = capacity && count[pass] < capacity && calls[pass] % every == 0;
+    if (open[pass]) (void)hipEventRecord(ev[pass][2 * count[pass]], st);
   }
   __host__ void end(int pass, int n_jobs, hipStream_t st) {
-    if (capacity && count[pass] < capacity) {
+    ++calls[pass];
+    if (open[pass]) {
       (void)hipEventRecord(ev[pass][2 * count[pass] + 1], st);
       ++count[pass];
       jobs[pass] += n_jobs;
+      open[pass] = false;
     }
   }
 };

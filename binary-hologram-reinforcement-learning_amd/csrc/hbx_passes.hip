@@ -76,20 +76,24 @@ using LayoutA = PanelLine<R, R * R / 2, pan_a(R)>;
 template <int R>
 using LayoutB = PanelLine<R, R * R, pan_b(R)>;
 
-// B at N = 1024 (r03): 1-KB tiles [y / 16][s / 8][16 rows][8 slots] of the line SLOT
+// B at N = 1024 and 256 (r03): tiles [y / 16][s / TL][16 rows][TL slots], TL = 256 / R
+// (1 KB at N = 1024, 2 KB at N = 256), of the line SLOT
 //   s(kx) = kx (kx <= N/2),  3N/2 - kx (kx > N/2),
-// so the two output line sets of a k_col2 block -- lines kx0..kx0+7 and their mirrors
-// N - kx0 - 7 .. N - kx0 (N/2 for kx = 0) -- each fill one aligned tile, which the block
-// writes as one contiguous KB per 16-row band (staged through LDS), and a k_rowinv block
-// (8 rows) reads 512-B runs.  Replayed without arithmetic (tools/membw3.hip): k_col2's
-// movement 2.43 ms (today's 16-row panels 2.47), k_rowinv's 1.37 ms (1.62): DESIGN.md 4.
-struct TileB32 {
-  static constexpr int N = 1024;
-  __device__ static constexpr int line(int s) { return s <= N / 2 ? s : 3 * N / 2 - s; }
+// so the two output line sets of a k_col2 block -- its TL lines kx0 .. kx0 + TL - 1 and their
+// mirrors N - kx0 - TL + 1 .. N - kx0 (N/2 for kx = 0) -- each fill one aligned tile, which
+// the block writes as one contiguous run per 16-row band (staged through LDS), and a
+// k_rowinv_d block reads 64-B (N = 1024) / 128-B (N = 256) runs per row straight into its
+// FFT layout.  Replayed without arithmetic (tools/membw3.hip, N = 1024): k_col2's movement
+// 2.39-2.43 ms (16-row panels 2.41-2.47), k_rowinv's 1.37-1.40 ms (1.62-1.65): DESIGN.md 4.
+template <int R>
+struct TileB {
+  static constexpr int N = R * R, TL = 256 / R;
   __device__ static constexpr int at(int s, int y) {   // float2 offset of (slot s, row y)
-    return (((y >> 4) * (N / 8) + (s >> 3)) << 7) + ((y & 15) << 3) + (s & 7);
+    return (y >> 4) * 16 * N + (s / TL) * 16 * TL + (y & 15) * TL + s % TL;
   }
 };
+template <int R>
+constexpr bool kTiledB = R == 32 || R == 16;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
@@ -361,36 +365,44 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
 
-// N = 1024: the output line sets of a k_col2 block (8 lines: group g = slot g of slot
-// tile st, TileB32) go out through the FFT scratch.  col2_stage_write: each group
-// writes its line (imaginary part times sy) into its OWN scratch region (the group's
-// FFT is done with it; no block barrier), [band 64][row 16] at offset 4 g (a bank
-// shift that makes the readers' b64 loads conflict-free).  After a block barrier,
+// N = 1024 / 256: the output line sets of a k_col2 block (TL lines: group g = slot g of
+// slot tile st, TileB) go out through the FFT scratch.  col2_stage_write: each group
+// writes its line (imaginary part times sy) into its OWN scratch region (the group's FFT
+// is done with it; no block barrier) in row order, shifted by (g / 2) * 64 / TL float2 (the
+// bank shift that makes the readers' b64 loads conflict-free).  After a block barrier,
 // col2_stage_store: the block stores the set as 16-B chunks (slots 2 sp, 2 sp + 1 from
-// regions 2 sp, 2 sp + 1) in memory order -- one contiguous KB per 16-row band.
-__device__ __forceinline__ float2* col2_region(float2* scratch, int g) { return scratch + g * (32 * 33) + 4 * g; }
-
-__device__ __forceinline__ void col2_stage_write(const float2 (&v)[32], float sy, float2* scratch, int grp, int t) {
-  float2* reg = col2_region(scratch, grp);
-#pragma unroll
-  for (int k2 = 0; k2 < 32; ++k2) reg[32 * k2 + t] = make_float2(v[k2].x, sy * v[k2].y);   // (band, row) = y
+// regions 2 sp, 2 sp + 1) in memory order -- one contiguous run per 16-row band.
+template <int R>
+constexpr int col2_region_stride() { return R * (R + 1) > R * R + 32 ? R * (R + 1) : R * R + 32; }
+template <int R>
+__device__ __forceinline__ float2* col2_region(float2* scratch, int g) {
+  return scratch + g * col2_region_stride<R>() + (g >> 1) * (64 / (256 / R));
 }
 
-template <int SK>
-__device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
-  // chunk c = tid + 256 i: band c / 64 = tid / 64 + 4 i, row (c / 4) % 16 = (tid / 4) % 16, slot pair
-  // c % 4 = tid % 4; memory offset = lane part + (st * 128 + i * 65536) float2 (the latter in soffset)
-  const int tid = threadIdx.x, sp = tid & 3;
-  const int y0 = ((tid >> 6) << 4) + ((tid >> 2) & 15);
-  const float2* lo_r = col2_region(const_cast<float2*>(scratch), 2 * sp) + y0;
-  const float2* hi_r = col2_region(const_cast<float2*>(scratch), 2 * sp + 1) + y0;
-  const int voff = (((tid >> 6) << 14) + (((tid >> 2) & 15) << 3) + 2 * sp) * 8;
+template <int R>
+__device__ __forceinline__ void col2_stage_write(const float2 (&v)[R], float sy, float2* scratch, int grp, int t) {
+  float2* reg = col2_region<R>(scratch, grp);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float2 lo = store_round<SK>(lo_r[64 * i]);
-    const float2 hi = store_round<SK>(hi_r[64 * i]);
+  for (int k2 = 0; k2 < R; ++k2) reg[R * k2 + t] = make_float2(v[k2].x, sy * v[k2].y);   // row y = t + R k2
+}
+
+template <int R, int SK>
+__device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
+  constexpr int N = R * R, TL = 256 / R, CH = N * TL / 2;   // 16-B chunks per line set
+  // chunk c = tid + 256 i: band c / (8 TL) = tid / (8 TL) + (32 / TL) i, row (tid / (TL / 2)) % 16,
+  // slot pair tid % (TL / 2); memory offset = lane part + i (32 / TL) 16 N + st 16 TL (soffset)
+  const int tid = threadIdx.x, sp = tid % (TL / 2);
+  const int band0 = tid / (8 * TL), r = (tid / (TL / 2)) % 16;
+  const int y0 = band0 * 16 + r;
+  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + y0;
+  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + y0;
+  const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
+#pragma unroll
+  for (int i = 0; i < CH / 256; ++i) {
+    const float2 lo = store_round<SK>(lo_r[(32 / TL) * 16 * i]);
+    const float2 hi = store_round<SK>(hi_r[(32 / TL) * 16 * i]);
     const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
-    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 128 + i * 65536) * 8, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, 0);
   }
 }
 
@@ -406,7 +418,8 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   constexpr int LB = (N / 2) / (GPB * ITER);
   static_assert((N / 2) % (GPB * ITER) == 0, "line blocking");
   __shared__ float2 tw[N];
-  __shared__ float2 scratch[GPB * R * (R + 1)];
+  constexpr int RS = kTiledB<R> ? col2_region_stride<R>() : R * (R + 1);   // per-group scratch region
+  __shared__ float2 scratch[GPB * RS];
 
   for (int i = threadIdx.x; i < N; i += 256) tw[i] = tw_glob[i];
 
@@ -426,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
   // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
-  const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+  const PaddedScratch<R> sc{scratch + grp * RS};
   // the LB blocks of a plane run side by side: at iteration it they hold lines
   // it * LB * GPB + [0, LB * GPB), i.e. whole contiguous stretches of every panel
   constexpr int KSTEP = LB * GPB;
@@ -445,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * N + t) * 8;
-    if constexpr (R == 32) {
+    if constexpr (kTiledB<R>) {
       fft_group_s1<R, false, true>(v, t, tw);
       if (it > 0) lds_barrier();   // the previous iteration's second set has been read out
       fft_group_s2<R, false, true>(v, t, sc);
@@ -478,11 +491,11 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     }
     fft_group<R, true, true>(v, t, sc, tw);
     const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
-    if constexpr (R == 32) {
-      const int kxb = kx - grp;            // the block's 8 lines: slot tile kxb / 8
-      col2_stage_write(v, 1.0f, scratch, grp, t);
+    if constexpr (kTiledB<R>) {
+      const int kxb = kx - grp;            // the block's GPB lines: slot tile kxb / GPB
+      col2_stage_write<R>(v, 1.0f, scratch, grp, t);
       lds_barrier();
-      col2_stage_store<SK>(scratch, rb, kxb >> 3);
+      col2_stage_store<R, SK>(scratch, rb, kxb / GPB);
       if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
         const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
@@ -491,9 +504,9 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       fft_group_s1<R, true, true>(w, t, tw);
       lds_barrier();   // the first set has been read out: the regions are the FFTs' again
       fft_group_s2<R, true, true>(w, t, sc);
-      col2_stage_write(w, sy, scratch, grp, t);
+      col2_stage_write<R>(w, sy, scratch, grp, t);
       lds_barrier();
-      col2_stage_store<SK>(scratch, rb, (N / 2 + kxb) >> 3);
+      col2_stage_store<R, SK>(scratch, rb, (N / 2 + kxb) / GPB);
     } else {
       {
         const int vo = PB::voff(t, kx);
@@ -565,20 +578,23 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
   }
 }
 
-// k_rowinv at N = 1024 (r03): every lane loads its own FFT input straight from the
-// tiled B (TileB32) -- lane t of group g (row y0 + g) needs kx = t + 32 jj, which for
-// 8 consecutive lanes is 8 consecutive slots of one tile row (64 B; the two rows of a wave
-// are adjacent: 128 B), so no LDS tile and no block barrier sit in the plane loop: the
-// group's FFT transpose (wave_sync) is its only LDS traffic.  Two register sets
-// alternate by plane, the next plane's loads in flight under this plane's FFT.  The
-// r02 kernel staged each plane through a 64-KB LDS tile between three block barriers.
-__global__ __launch_bounds__(256, 2) void k_rowinv32(const JobDesc* __restrict__ jobs,
+// k_rowinv at N = 1024 / 256 (r03): every lane loads its own FFT input straight from
+// the tiled B (TileB) -- lane t of group g (row y0 + g) needs kx = t + R jj, which for TL
+// consecutive lanes is TL consecutive slots of one tile row (64 B at N = 1024: the two rows
+// of a wave are adjacent, 128 B; 128 B at N = 256: a wave's four rows are one 512-B run),
+// so no LDS tile and no block barrier sit in the plane loop: the group's FFT transpose
+// (wave_sync) is its only LDS traffic.  The next plane's loads are issued as soon as this
+// plane's FFT is done (two blocks per CU cover them; a second register set for a plane in
+// flight took one block per CU and measured 1.80 ms against 1.47).  The r02
+// kernel staged every plane through an LDS tile between three block barriers (1.80 ms).
+template <int R>
+__global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__ jobs,
                                                      const float2* __restrict__ ws_b,
                                                      const float* __restrict__ target,
                                                      const float2* __restrict__ tw_glob, int P, int G,
                                                      double* __restrict__ partial, float* __restrict__ inten_out,
                                                      float2* __restrict__ field_out, size_t tmask, int inten_by_env) {
-  constexpr int R = 32, N = 1024, GPB = 8, RB = N / GPB;
+  constexpr int N = R * R, GPB = 256 / R, RB = N / GPB, TL = 256 / R;
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
   __shared__ double red[GPB][3];
@@ -600,21 +616,23 @@ __global__ __launch_bounds__(256, 2) void k_rowinv32(const JobDesc* __restrict__
   const int y = rb * GPB + grp;
   constexpr int PLB = N * N;                 // float2 per B plane
   const __amdgpu_buffer_rsrc_t rs = plane_rsrc(ws_b + (size_t)j * P * PLB, (unsigned)((size_t)P * PLB * 8));
-  // lane bases (bytes) of this row: slot s of row y at TileB32::at(s, y).
-  //   jj < 16 (and kx = 512 for t = 0): s = kx = t + 32 jj -> lo + 4096 jj
-  //   jj >= 16 otherwise: s = 3N/2 - kx = 1536 - t - 32 jj -> hi - 4096 jj, written as
-  //   hi31 + 4096 (31 - jj) so every offset stays non-negative
-  const int yb = ((y >> 4) << 14) + ((y & 15) << 3);
-  const int m = t >> 3, u = t & 7;
-  const int lo = (yb + (m << 7) + u) * 8;
-  const int hi31 = (yb + (u ? ((191 - m) << 7) + 8 - u : (192 - m) << 7) - 512 * 31) * 8;
-  const int v16 = t == 0 ? lo + 4096 * 16 : hi31 + 4096 * 15;
+  // lane bases (bytes) of this row, slot s at TileB<R>::at(s, y):
+  //   jj < R/2 (and kx = N/2 for t = 0): s = kx = t + R jj -> lo + 16 R jj float2
+  //   jj >= R/2 otherwise: s = 3N/2 - kx -> hi - 16 R jj, written hiB + 16 R (R - 1 - jj)
+  //   so every offset stays non-negative
+  constexpr int JS = 16 * R * 8;             // bytes per jj
+  const int yb = (y >> 4) * 16 * N + (y & 15) * TL;
+  const int m = t / TL, u = t % TL;
+  const int lo = (yb + m * 16 * TL + u) * 8;
+  const int hiB = (yb + (u ? (3 * N / (2 * TL) - m - 1) * 16 * TL + TL - u : (3 * N / (2 * TL) - m) * 16 * TL) -
+                   16 * R * (R - 1)) * 8;
+  const int vmid = t == 0 ? lo + JS * (R / 2) : hiB + JS * (R / 2 - 1);
   auto load_plane = [&](pk2 (&v)[R], int p) {
     const int po = p * PLB * 8;
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) {
-      const int vo = jj < 16 ? lo : (jj == 16 ? v16 : hi31);
-      const int so = po + (jj < 16 ? 4096 * jj : (jj == 16 ? 0 : 4096 * (31 - jj)));
+      const int vo = jj < R / 2 ? lo : (jj == R / 2 ? vmid : hiB);
+      const int so = po + (jj < R / 2 ? JS * jj : (jj == R / 2 ? 0 : JS * (R - 1 - jj)));
       v[jj] = to_pk(buf_ld2s(rs, vo, so));
     }
   };
@@ -635,12 +653,22 @@ __global__ __launch_bounds__(256, 2) void k_rowinv32(const JobDesc* __restrict__
   pk2 va[R];
   load_plane(va, 0);
   __syncthreads();  // tw visible
+  if constexpr (R == 16) {   // N = 256: registers to spare -- the next plane in flight under this one's FFT
+    pk2 vb[R];
 #pragma unroll 1
-  for (int p = 0; p < P; ++p) {              // the next plane's loads issued as soon as this one's FFT is done
-    finish_plane(va, p);
-    load_plane(va, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
+    for (int p = 0; p < P; p += 2) {         // P is even (hbx_plan_create)
+      load_plane(vb, p + 1);
+      finish_plane(va, p);
+      load_plane(va, p + 2 < P ? p + 2 : p + 1);
+      finish_plane(vb, p + 1);
+    }
+  } else {
+#pragma unroll 1
+    for (int p = 0; p < P; ++p) {
+      finish_plane(va, p);
+      load_plane(va, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
+    }
   }
-
   rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
 }
 
@@ -898,8 +926,8 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
-    if constexpr (R == 32)
-      hipLaunchKernelGGL(k_rowinv32, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
+    if constexpr (kTiledB<R>)
+      hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
                          pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
                          pd.inten_by_env);
     else

@@ -30,7 +30,7 @@ OBS_STATE, OBS_RECON = 1, 2   # hbx_env_obs_sync
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
     "hbx_plan_workspace_bytes", "hbx_plan_pipeline", "hbx_propagate", "hbx_psnr", "hbx_env_reset", "hbx_env_step",
-    "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_read_timing",
+    "hbx_step", "hbx_eval_flips", "hbx_commit_flip", "hbx_plan_set_timing", "hbx_plan_set_timing_sampled", "hbx_plan_read_timing",
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
     "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
@@ -126,6 +126,7 @@ def _declare(lib):
     lib.hbx_plan_precision.argtypes = [VP]
     lib.hbx_env_obs_sync.argtypes = [VP, C.POINTER(EnvBuffers), I32, VP, I32, I32, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
+    lib.hbx_plan_set_timing_sampled.argtypes = [VP, I32, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                          C.POINTER(C.c_int64)]
     for name in EXPORTED_SYMBOLS:

@@ -328,9 +328,12 @@ class HologramVecEnv(_VecEnvBase):
     def step_wait(self):
         return self.step(self._actions)
 
-    def step_device(self, actions: torch.Tensor):
+    def step_device(self, actions: torch.Tensor, out=None):
         """One batched env.step (no host sync): returns device tensors
-        (reward f64, psnr f64, accepted u8, terminated u8, truncated u8)."""
+        (reward f64, psnr f64, accepted u8, terminated u8, truncated u8).
+        ``out``: five contiguous [B] device tensors of those dtypes the step
+        kernel writes instead of the env's own (e.g. hbx.dist.StepMetricGather.slot(),
+        so the metric gather needs no per-step packing); they are returned."""
         if not isinstance(actions, torch.Tensor) or actions.device != self.device \
                 or actions.dtype != torch.int64:
             actions = torch.as_tensor(np.asarray(actions, np.int64) if not isinstance(actions, torch.Tensor)
@@ -345,16 +348,24 @@ class HologramVecEnv(_VecEnvBase):
                                   (a[:, 0] * c.height + a[:, 1]) * c.width + a[:, 2])
         actions = actions.reshape(self.num_envs).contiguous()
         self._last_actions = actions
+        if out is None:
+            out = (self._reward, self._psnr, self._acc, self._term, self._trunc)
+        else:
+            out = tuple(out)
+            want = (torch.float64, torch.float64, torch.uint8, torch.uint8, torch.uint8)
+            if len(out) != 5 or any(not isinstance(t, torch.Tensor) or t.dtype != d or t.device != self.device
+                                    or t.numel() != self.num_envs or not t.is_contiguous()
+                                    for t, d in zip(out, want)):
+                raise ValueError("step_device out: five contiguous [B] device tensors "
+                                 "(f64 reward, f64 psnr, u8 accepted, u8 terminated, u8 truncated)")
         if self.mode == "psf":
-            self.plan.env_step_psf(self.state.bufs, self.params, self.num_envs, actions, self._reward,
-                                   self._psnr, self._acc, self._term, self._trunc)
+            self.plan.env_step_psf(self.state.bufs, self.params, self.num_envs, actions, *out)
             self._since_refresh += 1
             if self.refresh_every and self._since_refresh >= self.refresh_every:
                 self.refresh()
         else:
-            self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, self._reward,
-                               self._psnr, self._acc, self._term, self._trunc)
-        return self._reward, self._psnr, self._acc, self._term, self._trunc
+            self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, *out)
+        return out
 
     def refresh(self):
         """Exact FFT re-propagation of the cached fields (incremental mode)."""

@@ -169,8 +169,10 @@ class Plan:
         return int(self.lib.hbx_plan_workspace_bytes(self._h))
 
     # -- device timing of the three passes (hbx_plan_set_timing) --------------------
-    def set_timing(self, capacity: int):
-        _lib.check(self.lib.hbx_plan_set_timing(self._h, int(capacity)), "hbx_plan_set_timing")
+    def set_timing(self, capacity: int, every: int = 1):
+        """Record up to `capacity` launches per pass, every `every`-th launch."""
+        _lib.check(self.lib.hbx_plan_set_timing_sampled(self._h, int(capacity), int(every)),
+                   "hbx_plan_set_timing_sampled")
 
     def read_timing(self):
         """{pass: (total_ms, launches, jobs)} for k_rowfwd / k_col / k_rowinv (syncs)."""

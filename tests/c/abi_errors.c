@@ -61,6 +61,7 @@ int main(void) {
   CHECK(hbx_plan_set_precision(NULL, HBX_PRECISION_BF16_STORE) == HBX_ERR_INVALID);
   CHECK(hbx_plan_precision(NULL) == HBX_ERR_INVALID);
   CHECK(hbx_plan_set_timing(NULL, 4) == HBX_ERR_INVALID);
+  CHECK(hbx_plan_set_timing_sampled(NULL, 4, 2) == HBX_ERR_INVALID);
   CHECK(hbx_plan_read_timing(NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_plan_workspace_bytes(NULL) == 0);
   CHECK(hbx_plan_destroy(NULL) == HBX_OK);

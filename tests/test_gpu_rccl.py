@@ -32,7 +32,8 @@ def _run_all(tmp, tag):
     dev = torch.device("cuda", 0)
     ocfg, cfg = _inputs()
     out = {}
-    # per-step metric gather of a real 4-env VecEnv, 5 steps gathered every 3
+    # per-step metric gather of a real 4-env VecEnv, 5 steps gathered every 3; the step
+    # kernel writes its outputs straight into the gather's byte rows (slot())
     ins = [O.synthetic_inputs(ocfg, 40 + i) for i in range(4)]
     vec = HologramVecEnv(cfg, 4, lambda i: ins[i][1], pre_model_source=lambda i: ins[i][0],
                          obs_keys=(), auto_reset=False)
@@ -41,7 +42,9 @@ def _run_all(tmp, tag):
     mg = hd.StepMetricGather(4, every=3, device=dev)
     single = []
     for k in range(5):
-        r, ps, acc, term, trunc = vec.step_device(acts[k])
+        slot = mg.slot()
+        r, ps, acc, term, trunc = vec.step_device(acts[k], out=slot)
+        assert all(a.data_ptr() == b.data_ptr() for a, b in zip((r, ps, acc, term, trunc), slot))
         single.append(hd.gather_to_rank0(hd.pack_step_metrics(r, ps, acc, term, trunc)).cpu().numpy())
         mg.add(r, ps, acc, term, trunc)
     mg.flush()

@@ -256,6 +256,46 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_tiled(const float2* __restric
   if (acc == 12345.f) out[0] = acc;
 }
 
+// k_rowinv's direct lane loads (lane t of group g: kx = t + 32 jj, row y0 + g, 8 B) from
+// B in 16-row panels [y / 16][kx][16] -- no LDS tile, no barrier; two planes in flight
+__global__ __launch_bounds__(256, 2) void k_rowinv_direct_pan16(const float2* __restrict__ B, float* out) {
+  constexpr int G = 8, RB = N / G;
+  const int bid = xcd_group(blockIdx.x);
+  const int rb = bid % RB;
+  const int job = bid / RB;
+  const int grp = threadIdx.x / R, t = threadIdx.x % R;
+  const int y = rb * G + grp;
+  float acc = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float2* b = B + ((size_t)job * P + p) * N * N + (size_t)(y / 16) * N * 16 + y % 16;
+    float2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) v[jj] = b[(size_t)(t + R * jj) * 16];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) acc += v[jj].x + v[jj].y;
+  }
+  if (acc == 12345.f) out[0] = acc;
+}
+// the same from the 1-KB slot tiles (k_rowinv32's loads): kx = t + 32 jj, lower slots only (timing)
+__global__ __launch_bounds__(256, 2) void k_rowinv_direct_t8(const float2* __restrict__ B, float* out) {
+  constexpr int G = 8, RB = N / G;
+  const int bid = xcd_group(blockIdx.x);
+  const int rb = bid % RB;
+  const int job = bid / RB;
+  const int grp = threadIdx.x / R, t = threadIdx.x % R;
+  const int y = rb * G + grp;
+  float acc = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float2* b = B + ((size_t)job * P + p) * N * N;
+    float2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) v[jj] = b[tile_at<8>((t + R * jj) % N, y)];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) acc += v[jj].x + v[jj].y;
+  }
+  if (acc == 12345.f) out[0] = acc;
+}
+
 template <int PAN>
 __global__ __launch_bounds__(256, 2) void k_rowinv_rows(const float2* __restrict__ B, float* out) {
   constexpr int G = 8, RB = N / G, CH16 = N * G / 2;
@@ -328,6 +368,8 @@ int main() {
     time("col2_T16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<16>), gcol / 2, 512, 0, 0, A, B); });
     time("col2_T8_direct8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<false>), gcol, 256, 0, 0, A, B); });
     time("col2_T8_swap16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<true>), gcol, 256, 0, 0, A, B); });
+    time("rowinv_direct_pan16", (double)b_bytes, [&] { hipLaunchKernelGGL(k_rowinv_direct_pan16, jobs * (N / 8), 256, 0, 0, B, o); });
+    time("rowinv_direct_t8", (double)b_bytes, [&] { hipLaunchKernelGGL(k_rowinv_direct_t8, jobs * (N / 8), 256, 0, 0, B, o); });
     time("rowinv_T8", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_tiled<8>), jobs * (N / 8), 256, 0, 0, B, o); });
     time("rowinv_T16", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_tiled<16>), jobs * (N / 8), 256, 0, 0, B, o); });
   }
