@@ -245,11 +245,20 @@ class HologramVecEnv(_VecEnvBase):
             "target_image": spaces.Box(0, 1, (1, c.groups, c.height, c.width), np.float32),
         })
         n, dev = self.num_envs, self.device
-        self._reward = torch.zeros(n, dtype=torch.float64, device=dev)
-        self._psnr = torch.zeros(n, dtype=torch.float64, device=dev)
-        self._acc = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self._term = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self._trunc = torch.zeros(n, dtype=torch.uint8, device=dev)
+        # the step's outputs in ONE device byte row (reward f64 | psnr f64 | accepted, terminated,
+        # truncated u8 | error i32), so step() reads them back with one copy into pinned memory
+        self._row_bytes = -(-19 * n // 8) * 8
+        self._out_raw = torch.zeros(self._row_bytes + 8, dtype=torch.uint8, device=dev)
+        raw = self._out_raw
+        self._reward = raw[:8 * n].view(torch.float64)
+        self._psnr = raw[8 * n:16 * n].view(torch.float64)
+        self._acc, self._term, self._trunc = raw[16 * n:17 * n], raw[17 * n:18 * n], raw[18 * n:19 * n]
+        self.state.error = raw[self._row_bytes:self._row_bytes + 4].view(torch.int32)   # the kernels' error word
+        self.state.bufs.error = self.state.error.data_ptr()
+        self._host_raw = torch.zeros(self._row_bytes + 8, dtype=torch.uint8,
+                                     pin_memory=self.device.type == "cuda")
+        self._host_np = self._host_raw.numpy()
+        self._readback = torch.cuda.Event() if self.device.type == "cuda" else None
         self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
         self.episode_count = 0
@@ -376,20 +385,26 @@ class HologramVecEnv(_VecEnvBase):
     def step(self, actions):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
         (done envs report their last observation as info["terminal_observation"])."""
-        reward, psnr, acc, term, trunc = self.step_device(actions)
+        self.step_device(actions)
         n = self.num_envs
-        # one device -> host copy per step: rewards, done flags and the error word together
-        host = torch.cat([reward, term.double(), trunc.double(), self.state.error.double()]).cpu().numpy()
-        if host[3 * n] != 0:
-            self.state.check_error()                      # clears the word and raises
+        # one device -> pinned host copy per step (rewards, done flags, the error word), queued
+        # behind the step; the observation views and infos are built while it is in flight
+        self._host_raw.copy_(self._out_raw, non_blocking=True)
+        if self._readback is not None:
+            self._readback.record()
         obs = self.observe(stepped=True)
-        r = host[:n].copy()
+        infos = [{} for _ in range(self.num_envs)]
+        if self._readback is not None:
+            self._readback.synchronize()
+        h = self._host_np
+        if h[self._row_bytes:self._row_bytes + 4].view(np.int32)[0] != 0:
+            self.state.check_error()                      # clears the word and raises
+        r = h[:8 * n].view(np.float64).copy()
         if self.obs_format != "torch":
             r = r.astype(np.float32)
-        t = host[n:2 * n] != 0
-        tr = host[2 * n:3 * n] != 0
+        t = h[17 * n:18 * n] != 0
+        tr = h[18 * n:19 * n] != 0
         dones = t | tr
-        infos = [{} for _ in range(self.num_envs)]
         if self.auto_reset and dones.any():
             done_ids = np.nonzero(dones)[0].tolist()
             term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}

@@ -19,7 +19,10 @@ KERNELS = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
 
 def short(name):
     m = re.search(r"hbx::(k_[a-z_]+)", name)
-    return m.group(1) if m else None
+    if not m:
+        return None
+    k = m.group(1)
+    return k[:-2] if k.endswith("_d") else k     # k_rowinv_d (r03's direct-load variant) is the k_rowinv pass
 
 
 def load_counters(path):
