@@ -353,11 +353,12 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 // is even in fx and fy); inverse FFT of Z H -> B line kx.  H is even in ky, so
 //   IFFT_y(M H)(y) = conj IFFT_y(Z conj H)(y),   M(ky) = conj Z(-ky),
 // i.e. B line N - kx is the conjugate of the inverse FFT of W, formed in
-// registers from the same H values (no LDS mirror).  Only kx = 0 needs M itself
+// registers from the same H values (no LDS mirror of the line).  Only kx = 0 needs M itself
 // ((Z + M)/2 and (Z - M)/2 are the transforms of the two real lines packed into
 // A line 0: a register shuffle, mirror_conj; -> lines 0 and N/2).  One forward
-// FFT per input line, one A read, one H read; every LDS hand-off stays inside
-// the group's own scratch (wave_sync only).  The next line's loads go into v
+// FFT per input line, one A read, one read of half the H row (N = 1024 / 256: H is even
+// in ky, the other half comes mirrored through the group's scratch); the FFT and H hand-offs
+// stay inside the group's own scratch (wave_sync only).  The next line's loads go into v
 // as soon as line kx is stored and fly under the second inverse FFT.
 // Scalar-f32 FFTs: with two lines in registers the packed variant spills.
 // Measured and removed: the round-1 LDS mirror, packed DFTs,
@@ -458,25 +459,46 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * N + t) * 8;
+    // H(kx, .) of this line (N = 1024 / 256: the R/2 + 1 values of ky <= N/2 only, mirrored
+    // below), issued before the second FFT stage so the loads fly under it
+    constexpr int HP = kTiledB<R> ? R / 2 + 1 : 0;
+    float2 hb[R];
     if constexpr (kTiledB<R>) {
       fft_group_s1<R, false, true>(v, t, tw);
+      if (!dc) {
+#pragma unroll
+        for (int i = 0; i < HP; ++i) hb[i] = buf_ld2(rh, vh, i * R * 8);
+      }
       if (it > 0) lds_barrier();   // the previous iteration's second set has been read out
       fft_group_s2<R, false, true>(v, t, sc);
     } else {
       fft_group<R, false, true>(v, t, sc, tw);
     }
     float2 w[R];
-    if (!dc) {   // v <- Z H, w <- Z conj H, each H value consumed as it arrives
+    if (!dc) {   // v <- Z H, w <- Z conj H
+      if constexpr (kTiledB<R>) {
+        // H(kx, N - ky) = H(kx, ky): lane t holds ky = t + R k2, whose mirror N - ky sits on
+        // lane (R - t) mod R at k2' = R - 1 - k2 (lane 0: its own k2' = R - k2).  The group's
+        // loads of k2 <= R/2 go through its FFT scratch (free between the forward and the
+        // inverse FFT) and come back mirrored: 17 H loads per line instead of 32 at N = 1024,
+        // k_col2 2.67 -> 2.58 ms
+        float2* hs = scratch + grp * RS;
+        wave_sync();
 #pragma unroll
-      for (int c8 = 0; c8 < R; c8 += 8) {
-        float2 hb[8];
+        for (int i = 0; i <= R / 2; ++i) hs[i * R + t] = hb[i];
+        wave_sync();
+        const float2* hm = hs + (t == 0 ? R : 0) + ((R - t) & (R - 1));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * R * 8);
+        for (int i = R / 2 + 1; i < R; ++i) hb[i] = hm[(R - 1 - i) * R];
+        wave_sync();
+      } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          w[c8 + i] = cmulc(v[c8 + i], hb[i]);
-          v[c8 + i] = cmul(v[c8 + i], hb[i]);
-        }
+        for (int i = 0; i < R; ++i) hb[i] = buf_ld2(rh, vh, i * R * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        w[i] = cmulc(v[i], hb[i]);
+        v[i] = cmul(v[i], hb[i]);
       }
     } else {     // kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(N/2) -> line N/2
       const int vn = ((N / 2) * N + t) * 8;
