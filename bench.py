@@ -640,18 +640,26 @@ def main():
         # SURVEY 3.2 / BASELINE cfg 4's per-GPU shard: train-PPO.py's env (env.py, 256x256x8 mono),
         # 128 envs per GPU, FFT mode -- a secondary line, not the headline metric
         mono = mono_config(256)
-        vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup, mcfg=mono)
+        # a 0.35-ms step: 8x the headline's step count keeps the timed region ~0.1 s
+        msteps = 8 * args.steps
+        vec, dt, timing, acc_rate = measure("fft", msteps, args.warmup, mcfg=mono)
         ps = pass_table(timing, algorithmic_bytes(256, mono.planes))
         vec.close()
         if rank == 0:
             dom = max(ps, key=lambda n: ps[n]["avg_ms"])
-            mono_ms = dt / args.steps * 1e3
+            mono_ms = dt / msteps * 1e3
+            pmc = load_pmc_traffic(256)
+            mtraffic = None
+            if pmc and dom in pmc.get("kernels", {}):
+                kinfo = pmc["kernels"][dom]
+                if kinfo.get("jobs_per_launch") == ps[dom]["jobs_per_launch"] and kinfo.get("N") == 256:
+                    mtraffic = kinfo.get("hbm_bytes_per_launch")
             out["ppo_mono_256"] = {
-                "value": round(B * args.steps / dt, 2), "unit": "env-steps/s", "envs": B,
+                "value": round(B * msteps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": msteps,
                 "ms_per_step": round(mono_ms, 4), "accept_rate": round(acc_rate, 4),
                 "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ps[dom]["achieved_GBs"], 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ps[dom]["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                             "frac": round(ps[dom]["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": mtraffic,
                              "kernel_avg_ms": round(ps[dom]["avg_ms"], 4)},
                 "passes": rounded(ps),
                 "note": "configs[0] / train-PPO.py's env (env.py, 256x256, 1 colour group x 8 planes at 515 nm), "

@@ -149,15 +149,12 @@ int hbx_plan_create(hbx_plan_t* plan, const hbx_optics_t* optics, int32_t max_jo
 int hbx_plan_destroy(hbx_plan_t plan);
 size_t hbx_plan_workspace_bytes(hbx_plan_t plan);
 /* Propagation pipeline the plan runs (ABI v4): which kernels fill the pass
- * timer slots HBX_PASS_ROWFWD / HBX_PASS_COL below.
- *   HBX_PIPE_THREE_PASS  k_rowfwd -> k_col2 -> k_rowinv (N = 64, 256, 1024; the default)
- *   HBX_PIPE_COLBITS     N = 1024 with HBX_COLBITS=1 in the environment at plan creation:
- *                        k_bits_t -> k_colbits -> k_rowinv (no row-spectrum intermediate;
- *                        slots ROWFWD / COL time k_bits_t / k_colbits; measured slower)
- *   HBX_PIPE_GENERIC     N = 896: composed mixed-radix path */
+ * timer slots HBX_PASS_ROWFWD / HBX_PASS_COL below.  Since ABI v8 always
+ *   HBX_PIPE_THREE_PASS  k_rowfwd -> k_col2 -> k_rowinv (N = 64, 256, 896, 1024; N = 896 runs
+ *                        the fused mixed-radix 28 x 32 kernels of the same three passes)
+ * (the r01 / r02 bits -> column pass and composed generic-N pipelines, values 1 and 2, were
+ * measured slower and removed). */
 #define HBX_PIPE_THREE_PASS 0
-#define HBX_PIPE_COLBITS 1
-#define HBX_PIPE_GENERIC 2
 int hbx_plan_pipeline(hbx_plan_t plan);
 
 /* Full propagation of every group of n_env masks (env.py:123-133 reset path,
