@@ -66,6 +66,7 @@ struct hbx_plan {
   size_t walk_partial_elems = 0;
   int* walk_counter = nullptr;     // fused walk step: arrival tickets [9] (zero between launches)
   int walk_split = 0;              // HBX_WALK_SPLIT=1: three-launch batches for every K
+  int walk_persist = 0;            // HBX_WALK_PERSIST=1: one cooperative launch per walk call
 };
 
 namespace {
@@ -151,6 +152,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   {
     const char* ev = std::getenv("HBX_WALK_SPLIT");   // A/B switch: the v5 three-launch walk batches
     p->walk_split = (ev && ev[0] && ev[0] != '0') ? 1 : 0;
+    const char* ep = std::getenv("HBX_WALK_PERSIST");   // the persistent fused walk (r03, measured)
+    p->walk_persist = (ep && ep[0] && ep[0] != '0') ? 1 : 0;
   }
   const size_t hrow = (size_t)(N / 2 + 1) * N;
   std::vector<float2> ht((size_t)G * hrow);
@@ -848,6 +851,7 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   l.partial = p->walk_partial;
   l.counter = p->walk_counter;
   l.fused = p->walk_split ? 0 : 1;
+  l.persist = p->walk_persist;
   l.K = K;
   l.batches = batches;
   l.count = pixel_count(p);
@@ -856,6 +860,7 @@ int hbx_dbs_walk_psf(hbx_plan_t p, uint64_t* base_mask, const float* target, dou
   // the decoded next actions a previous launch left are keyed on (position, order
   // pointer); a new call may bring new order contents at the same address: invalidate
   HBX_HIP(hipMemsetAsync(p->walk_counter + hbx::kWalkCounters, 0xff, sizeof(int64_t), st));
+  HBX_HIP(hipMemsetAsync(p->walk_counter + hbx::kWalkAbort, 0, sizeof(int), st));   // persistent walk
   HBX_HIP(hbx::launch_walk(pd, l, st));
   return HBX_OK;
 }

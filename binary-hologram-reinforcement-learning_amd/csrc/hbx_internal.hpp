@@ -204,6 +204,7 @@ struct WalkLaunch {
   double* partial;   // split batch: [K][walk_blocks_per_job(N, K)][2]; fused step: [blocks][terms]
   int* counter;      // fused step: walk scratch (kWalkScratchBytes): tickets, then WalkPre
   int fused;         // 1: one k_walk_step launch per batch when K has a fused variant
+  int persist;       // 1 (with fused): one cooperative launch runs all `batches` (grid barrier per batch)
   int K, batches;
   double count, peak;
   int rel;
@@ -217,6 +218,9 @@ constexpr int kWalkStepMaxTerms = 26;   // 2 K + 3 K (K-1) / 2 at K = 4: max ove
 // zero between launches), then the WalkPre the deciding block leaves for the next launch
 constexpr int kWalkCounters = 16;
 constexpr int kWalkTickets = 9;
+constexpr int kWalkGen = 12;             // persistent walk: generation word (bumped per decided batch)
+constexpr int kWalkAbort = 13;           //   and the abort word (a grid barrier timed out)
+constexpr unsigned kWalkSpinMax = 1u << 20;   // polls (each ~1-2 us) before a waiting block gives up
 constexpr int kWalkPreMax = 4;          // the largest fused K
 struct WalkPre {
   int64_t pos;              // valid for this walk position (-1: invalid; cleared per API call)

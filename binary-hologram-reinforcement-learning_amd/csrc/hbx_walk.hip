@@ -377,8 +377,8 @@ struct WalkCand {
 };
 
 
-template <int K, bool TWO>
-__global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restrict__ counter) {
+template <int K, bool TWO, bool PERSIST>
+__global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restrict__ counter, int n_batches) {
   constexpr int NP = TWO ? K * (K - 1) / 2 : 0;
   constexpr int NT = 2 * K + 3 * NP;
   constexpr int NG = HBX_MAX_GROUPS;
@@ -393,6 +393,30 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   __shared__ WalkCand s_cd[K];           // the decider's candidates, indexed at run time
   hbx_dbs_walk_t* w = a.w;
   WalkPre* prep = reinterpret_cast<WalkPre*>(counter + kWalkCounters);
+  // PERSIST (r03): the launch runs up to n_batches batches; between batches the grid meets at
+  // a barrier -- the last-arriving block decides, writes the walk state write-through and bumps
+  // the generation word the others spin on (bounded: a block that waits past kWalkSpinMax polls
+  // raises the abort word and the fault / done flags, and every waiting block leaves)
+  int* const gen = counter + kWalkGen;
+  int* const abort_word = counter + kWalkAbort;
+  __shared__ int s_gen, s_stop;
+  if constexpr (PERSIST) {
+    if (threadIdx.x == 0) s_gen = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const __amdgpu_buffer_rsrc_t r_ws = wave_rsrc(w, (unsigned)sizeof(hbx_dbs_walk_t));
+  const __amdgpu_buffer_rsrc_t r_pre = wave_rsrc(prep, (unsigned)sizeof(WalkPre));
+  const __amdgpu_buffer_rsrc_t r_mask = wave_rsrc(a.mask, 0xffffffffu);
+  const __amdgpu_buffer_rsrc_t r_bs = wave_rsrc(a.base_stats, (unsigned)(3 * HBX_MAX_GROUPS * sizeof(double)));
+  // mask words and base statistics: written by the deciding block of an earlier batch, which may
+  // sit on another XCD -- in a persistent launch they are read past the local L2 (sc1)
+  auto ld_mask = [&](size_t word) -> uint64_t {
+    if constexpr (PERSIST)
+      return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r_mask, (int)(word * 8), 0, kSc1));
+    else
+      return a.mask[word];
+  };
+#pragma unroll 1
+  for (int bb = 0; bb < (PERSIST ? n_batches : 1); ++bb) {
 #ifdef HBX_WALK_TIMING
   uint64_t tt[12];
   tt[0] = __builtin_amdgcn_s_memrealtime();
@@ -409,10 +433,20 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   static_assert(kWsWords + kPreWords <= 64, "one wave");
   __shared__ hbx_dbs_walk_t s_ws;
   __shared__ WalkPre s_pre;
-  if ((int)threadIdx.x < kWsWords)
-    reinterpret_cast<int*>(&s_ws)[threadIdx.x] = reinterpret_cast<const int*>(w)[threadIdx.x];
-  else if ((int)threadIdx.x < kWsWords + kPreWords)
-    reinterpret_cast<int*>(&s_pre)[threadIdx.x - kWsWords] = reinterpret_cast<const int*>(prep)[threadIdx.x - kWsWords];
+  if constexpr (PERSIST) {
+    __syncthreads();   // the previous batch's readers of s_ws / s_pre / s_cd are done
+    if ((int)threadIdx.x < kWsWords)
+      reinterpret_cast<int*>(&s_ws)[threadIdx.x] =
+          __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(r_ws, (int)threadIdx.x * 4, 0, kSc1));
+    else if ((int)threadIdx.x < kWsWords + kPreWords)
+      reinterpret_cast<int*>(&s_pre)[threadIdx.x - kWsWords] = __builtin_bit_cast(
+          int, __builtin_amdgcn_raw_buffer_load_b32(r_pre, ((int)threadIdx.x - kWsWords) * 4, 0, kSc1));
+  } else {
+    if ((int)threadIdx.x < kWsWords)
+      reinterpret_cast<int*>(&s_ws)[threadIdx.x] = reinterpret_cast<const int*>(w)[threadIdx.x];
+    else if ((int)threadIdx.x < kWsWords + kPreWords)
+      reinterpret_cast<int*>(&s_pre)[threadIdx.x - kWsWords] = reinterpret_cast<const int*>(prep)[threadIdx.x - kWsWords];
+  }
   __syncthreads();
   const hbx_dbs_walk_t ws = s_ws;
   const WalkPre pre = s_pre;
@@ -446,7 +480,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     if (use_pre) {
       cm[c].delta = pre.cdelta[c];
     } else {
-      const uint64_t wd = a.mask[((size_t)ch * N + cm[c].r) * (N / 64) + cm[c].col / 64];
+      const uint64_t wd = ld_mask(((size_t)ch * N + cm[c].r) * (N / 64) + cm[c].col / 64);
       cm[c].delta = a.vb * (float)(2 * (int)((wd >> (cm[c].col & 63)) & 1ull) - 1);   // after the flip
     }
   }
@@ -467,7 +501,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     if (use_pre) {
       cd[j].delta = pre.delta[j];
     } else {
-      const uint64_t wd = a.mask[((size_t)ch * N + cd[j].r) * (N / 64) + cd[j].col / 64];
+      const uint64_t wd = ld_mask(((size_t)ch * N + cd[j].r) * (N / 64) + cd[j].col / 64);
       cd[j].delta = a.vb * (float)(1 - 2 * (int)((wd >> (cd[j].col & 63)) & 1ull));   // before the flip
     }
   }
@@ -635,7 +669,36 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     s_last = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) {
+    if constexpr (!PERSIST) {
+      return;
+    } else {
+      // wait for the deciding block's generation bump (bounded; see above)
+      if (threadIdx.x == 0) {
+        int stop = 0;
+        unsigned polls = 0;
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == s_gen) {
+          if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { stop = 1; break; }
+          if (++polls > kWalkSpinMax) {
+            __hip_atomic_store(abort_word, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the walk state is unreliable from here: fault + done stop the caller
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, 1), r_ws,
+                                                  (int)offsetof(hbx_dbs_walk_t, fault), 0, kSc1);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, 1), r_ws,
+                                                  (int)offsetof(hbx_dbs_walk_t, done), 0, kSc1);
+            stop = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        s_stop = stop;
+        s_gen = s_gen + 1;
+      }
+      __syncthreads();
+      if (s_stop) return;
+      continue;
+    }
+  }
   HBX_TT(4);
 
   // ---- the last block: every partial (fixed order), the PSNRs, the decision ----
@@ -646,11 +709,16 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   if (tid < nn && nact >= 0 && nact < (int64_t)CH * (int64_t)hw) {
     nch = (int)(nact / (int64_t)hw);
     npix = (int)(nact % (int64_t)hw);
-    nwd = a.mask[((size_t)nch * N + npix / N) * (N / 64) + (npix % N) / 64];
+    nwd = ld_mask(((size_t)nch * N + npix / N) * (N / 64) + (npix % N) / 64);
   }
   double bs[3 * NG];
 #pragma unroll
-  for (int i = 0; i < 3 * NG; ++i) bs[i] = i < 3 * G ? a.base_stats[i] : 0.0;
+  for (int i = 0; i < 3 * NG; ++i) {
+    if constexpr (PERSIST)
+      bs[i] = i < 3 * G ? __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r_bs, i * 8, 0, kSc1)) : 0.0;
+    else
+      bs[i] = i < 3 * G ? a.base_stats[i] : 0.0;
+  }
   double v[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) v[t] = 0.0;
@@ -728,7 +796,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     s_ps[tid] = ps;
   }
   __syncthreads();
-  if (tid != 0) return;
+  if (tid == 0) {
   HBX_TT(9);
   HBX_TT(10);
   for (int i = 0; i < kWalkTickets; ++i)
@@ -796,8 +864,13 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
         const int j = acc_j[s2];
         if (j < 0) break;
         const WalkCand cj = s_cd[j];
-        atomicXor(reinterpret_cast<unsigned long long*>(a.mask) + ((size_t)cj.ch * N + cj.r) * (N / 64) + cj.col / 64,
-                  1ull << (cj.col & 63));                                         // DBS_1024_24.py:320
+        const size_t mw = ((size_t)cj.ch * N + cj.r) * (N / 64) + cj.col / 64;
+        if constexpr (PERSIST) {   // the only writer of the mask while the walk runs: plain RMW, write-through
+          const uint64_t nv = ld_mask(mw) ^ (1ull << (cj.col & 63));                 // DBS_1024_24.py:320
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(walk_u32x2, nv), r_mask, (int)(mw * 8), 0, kSc1);
+        } else {
+          atomicXor(reinterpret_cast<unsigned long long*>(a.mask) + mw, 1ull << (cj.col & 63));   // DBS_1024_24.py:320
+        }
         const int64_t n = ws.accepted + s2;
         if (n < a.log_cap) {
           a.log_pos[n] = pos + j;
@@ -808,7 +881,12 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
       }
 #pragma unroll
       for (int i = 0; i < 3 * NG; ++i)
-        if (i < 3 * G) a.base_stats[i] = fin[i];                                   // :358-363
+        if (i < 3 * G) {                                                           // :358-363
+          if constexpr (PERSIST)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(walk_u32x2, fin[i]), r_bs, i * 8, 0, kSc1);
+          else
+            a.base_stats[i] = fin[i];
+        }
     }
     nw.accepted = n_acc;
     nw.prev_psnr = prev;
@@ -847,8 +925,15 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     np.cdelta[s2] = acc_j[s2] >= 0 ? s_cd[acc_j[s2]].delta : 0.0f;   // vb (2 bit' - 1) = vb (1 - 2 bit)
-  *prep = np;
-  *w = nw;
+  if constexpr (PERSIST) {   // write-through: the next batch's blocks read them with sc1 loads
+    for (int i = 0; i < kPreWords; ++i)
+      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&np)[i], r_pre, i * 4, 0, kSc1);
+    for (int i = 0; i < kWsWords; ++i)
+      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&nw)[i], r_ws, i * 4, 0, kSc1);
+  } else {
+    *prep = np;
+    *w = nw;
+  }
 #ifdef HBX_WALK_TIMING
   HBX_TT(7);
   if (nw.batches % 500 == 7) {
@@ -874,6 +959,20 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     }
   }
 #endif
+  }   // tid == 0
+  if constexpr (!PERSIST) {
+    return;
+  } else {
+    if (tid == 0) {
+      // every write-through store of the decision (mask word, statistics, state, next actions,
+      // ticket reset) retired before the generation bump releases the other blocks
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(gen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_gen = s_gen + 1;
+    }
+    __syncthreads();
+  }
+  }   // batch loop
 }
 
 // blocks per candidate: enough blocks in flight to stream at full rate for
@@ -925,12 +1024,29 @@ hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
   const int nq = pd.N * pd.N / 4;
   const dim3 grid((unsigned)walk_step_blocks(pd.N));
   if (l.fused && walk_fused_k(l.K)) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cap);   // graph capture: per-batch launches (no cooperative node)
+    if (l.persist && l.batches > 1 && cap == hipStreamCaptureStatusNone) {
+      // one cooperative launch for the whole call (co-residency of the grid guaranteed, or the
+      // launch fails and the call falls back to one launch per batch below)
+      int nb = l.batches;
+      void* args[] = {&a, (void*)&l.counter, &nb};
+      const void* fn = nullptr;
+      switch (l.K) {
+        case 1: fn = reinterpret_cast<const void*>(&k_walk_step<1, false, true>); break;
+        case 2: fn = reinterpret_cast<const void*>(&k_walk_step<2, true, true>); break;
+        case 3: fn = reinterpret_cast<const void*>(&k_walk_step<3, true, true>); break;
+        default: fn = reinterpret_cast<const void*>(&k_walk_step<4, true, true>); break;
+      }
+      if (hipLaunchCooperativeKernel(fn, grid, dim3(kWalkNT), args, 0, st) == hipSuccess) return hipSuccess;
+      (void)hipGetLastError();
+    }
     for (int b = 0; b < l.batches; ++b) {
       switch (l.K) {
-        case 1: hipLaunchKernelGGL((k_walk_step<1, false>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
-        case 2: hipLaunchKernelGGL((k_walk_step<2, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
-        case 3: hipLaunchKernelGGL((k_walk_step<3, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
-        default: hipLaunchKernelGGL((k_walk_step<4, true>), grid, dim3(kWalkNT), 0, st, a, l.counter); break;
+        case 1: hipLaunchKernelGGL((k_walk_step<1, false, false>), grid, dim3(kWalkNT), 0, st, a, l.counter, 1); break;
+        case 2: hipLaunchKernelGGL((k_walk_step<2, true, false>), grid, dim3(kWalkNT), 0, st, a, l.counter, 1); break;
+        case 3: hipLaunchKernelGGL((k_walk_step<3, true, false>), grid, dim3(kWalkNT), 0, st, a, l.counter, 1); break;
+        default: hipLaunchKernelGGL((k_walk_step<4, true, false>), grid, dim3(kWalkNT), 0, st, a, l.counter, 1); break;
       }
     }
     return hipGetLastError();
@@ -941,7 +1057,7 @@ hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
     // are): one commit-only step, which returns at once when there are none
     WalkArgs c = a;
     c.commit_only = 1;
-    hipLaunchKernelGGL((k_walk_step<1, false>), grid, dim3(kWalkNT), 0, st, c, l.counter);
+    hipLaunchKernelGGL((k_walk_step<1, false, false>), grid, dim3(kWalkNT), 0, st, c, l.counter, 1);
   }
   for (int b = 0; b < l.batches; ++b) {
     hipLaunchKernelGGL(k_walk_eval, dim3((unsigned)a.bpj, (unsigned)l.K), dim3(kWalkNT), 0, st, a);

@@ -68,7 +68,7 @@ class DbsWalk(C.Structure):
         ("stop_enabled", C.c_int32), ("refresh_every", C.c_int32), ("done", C.c_int32), ("halt", C.c_int32),
         ("stopped_early", C.c_int32), ("commit_ch", C.c_int32), ("commit_pix", C.c_int32),
         ("commit2_ch1", C.c_int32), ("commit_pix2", C.c_int32), ("split_ch1", C.c_int32),
-        ("split_pix", C.c_int32), ("reserved", C.c_int32),
+        ("split_pix", C.c_int32), ("fault", C.c_int32),
     ]
 
 

@@ -279,7 +279,11 @@ class _Walk:
         slot = self.done_n % 2
         self.events[slot].synchronize()
         self.done_n += 1
-        return _lib.DbsWalk.from_buffer_copy(self.pinned[slot].numpy().tobytes())
+        st = _lib.DbsWalk.from_buffer_copy(self.pinned[slot].numpy().tobytes())
+        if st.fault:   # a persistent walk launch's grid barrier timed out (hbx.h: fault)
+            raise RuntimeError("hbx_dbs_walk_psf: persistent walk barrier timed out; walk state unreliable "
+                               "(rerun with HBX_WALK_PERSIST=0)")
+        return st
 
     def advance(self):
         """Wait for the oldest chunk in flight, act on its state, refill."""

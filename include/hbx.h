@@ -323,7 +323,8 @@ typedef struct hbx_dbs_walk {
   int32_t split_ch1;       /* internal (ABI v7): channel + 1 of the split batch's
                               accept, applied within the batch, 0 = none          */
   int32_t split_pix;       /* internal                                           */
-  int32_t reserved;        /* zero                                               */
+  int32_t fault;           /* (r03) 1: a persistent walk launch's grid barrier timed
+                              out (done is set too; the state is unreliable)     */
 } hbx_dbs_walk_t;
 int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
                      double* base_chan_stats, float* field, float* intensity, const int64_t* order,

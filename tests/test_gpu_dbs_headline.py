@@ -138,12 +138,15 @@ def test_incremental_greedy_1024x24_equals_oracle(golden_dir, name, mode, refres
     plan.close()
 
 
+@pytest.mark.parametrize("persist", ["0", "1"])
 @pytest.mark.parametrize("refresh", [4096, 256])
-def test_incremental_greedy_1024x24_16k_equals_oracle(golden_dir, refresh):
+def test_incremental_greedy_1024x24_16k_equals_oracle(golden_dir, refresh, persist, monkeypatch):
     """The device walk over a 16,384-candidate prefix of the 1024x24 sweep (the float64
     oracle's run, dbs_prefix_1024x24_16k.npz): every decision the oracle's, with and
-    without exact refreshes."""
+    without exact refreshes, with one launch per batch and with the persistent walk
+    (HBX_WALK_PERSIST=1: one cooperative launch per call, a grid barrier per batch)."""
     from hbx import dbs
+    monkeypatch.setenv("HBX_WALK_PERSIST", persist)   # read at plan creation
     d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
     n = int(d["n"])
     plan, mask, target = _dev(ocfg, pre, tgt)
