@@ -689,7 +689,7 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
             stop = 1;
             break;
           }
-          __builtin_amdgcn_s_sleep(2);
+          __builtin_amdgcn_s_sleep(8);
         }
         s_stop = stop;
         s_gen = s_gen + 1;
@@ -865,12 +865,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
         if (j < 0) break;
         const WalkCand cj = s_cd[j];
         const size_t mw = ((size_t)cj.ch * N + cj.r) * (N / 64) + cj.col / 64;
-        if constexpr (PERSIST) {   // the only writer of the mask while the walk runs: plain RMW, write-through
-          const uint64_t nv = ld_mask(mw) ^ (1ull << (cj.col & 63));                 // DBS_1024_24.py:320
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(walk_u32x2, nv), r_mask, (int)(mw * 8), 0, kSc1);
-        } else {
-          atomicXor(reinterpret_cast<unsigned long long*>(a.mask) + mw, 1ull << (cj.col & 63));   // DBS_1024_24.py:320
-        }
+        // device-scope atomic, performed past the XCD L2s (the persistent walk's readers load
+        // mask words with sc1; tests/test_gpu_parity.py::test_walk_repeated_positions_* revisits them)
+        atomicXor(reinterpret_cast<unsigned long long*>(a.mask) + mw, 1ull << (cj.col & 63));   // DBS_1024_24.py:320
         const int64_t n = ws.accepted + s2;
         if (n < a.log_cap) {
           a.log_pos[n] = pos + j;
@@ -925,11 +922,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
     np.cdelta[s2] = acc_j[s2] >= 0 ? s_cd[acc_j[s2]].delta : 0.0f;   // vb (2 bit' - 1) = vb (1 - 2 bit)
-  if constexpr (PERSIST) {   // write-through: the next batch's blocks read them with sc1 loads
-    for (int i = 0; i < kPreWords; ++i)
-      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&np)[i], r_pre, i * 4, 0, kSc1);
-    for (int i = 0; i < kWsWords; ++i)
-      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&nw)[i], r_ws, i * 4, 0, kSc1);
+  if constexpr (PERSIST) {   // staged: the block's lanes store them write-through below, one word each
+    s_ws = nw;
+    s_pre = np;
   } else {
     *prep = np;
     *w = nw;
@@ -963,10 +958,17 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   if constexpr (!PERSIST) {
     return;
   } else {
+    __syncthreads();
+    if (tid < kWsWords)
+      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&s_ws)[tid], r_ws, tid * 4, 0, kSc1);
+    else if (tid < kWsWords + kPreWords)
+      __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&s_pre)[tid - kWsWords], r_pre,
+                                            (tid - kWsWords) * 4, 0, kSc1);
+    // every write-through store and atomic of the decision (mask word, statistics, state, next
+    // actions, ticket reset) retired before the generation bump releases the other blocks
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (tid == 0) {
-      // every write-through store of the decision (mask word, statistics, state, next actions,
-      // ticket reset) retired before the generation bump releases the other blocks
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(gen, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_gen = s_gen + 1;
     }

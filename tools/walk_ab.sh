@@ -1,14 +1,13 @@
 #!/bin/bash
-# A/B of the device DBS walk (bench.py's 65,536-candidate prefix) between builds of libhbx, e.g.
-#   bash tools/walk_ab.sh libhbx libhbx_exp_<NAME> libhbx libhbx_exp_<NAME>   (csrc: make exp EXP=<NAME>)
-# (profiles/r01_walk_eval_ab.txt came from a one-pixel-per-lane k_walk_eval build, since reverted.)
-# Run ON the GPU box.
+# Persistent vs per-batch fused DBS walk on the bench's 65,536-candidate 1024x24 prefix
+# (run ON the GPU box from the repo root): bash tools/walk_ab.sh TAG
 set -o pipefail
-L=binary-hologram-reinforcement-learning_amd/hbx
-mkdir -p gpurun_out/walkab
-for lib in ${*:-libhbx libhbx}; do
-  HBX_LIB=$PWD/$L/$lib.so timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-psf --no-ppo --no-probe --cpu-sample 0 --no-psnr-check > gpurun_out/walkab/$lib.json 2> gpurun_out/walkab/$lib.err || exit 1
+T=${1:-wab}
+mkdir -p gpurun_out/$T
+Q="--steps 2 --warmup 1 --no-psf --no-probe --no-precision --no-ppo --no-obs --cpu-sample 0 --no-psnr-check"
+for p in 0 1 0 1; do
+  HBX_WALK_PERSIST=$p timeout -k 10 300 python bench.py $Q > gpurun_out/$T/p$p.json 2> gpurun_out/$T/p$p.err || exit 1
   python -c "
-import json; d = json.load(open('gpurun_out/walkab/$lib.json'))['dbs_greedy']['incremental_mode']
-print('%-28s %9.0f candidates/s  %.3f s  accepted %d' % ('$lib', d['flips_per_s'], d['seconds'], d['accepted']))"
+import json; d = json.loads(open('gpurun_out/$T/p$p.json').read().splitlines()[-1]); g = d['dbs_greedy']['incremental_mode']
+print('persist $p', g['flips_per_s'], g['batches'], g.get('several_images', {}).get('flips_per_s_aggregate'), g['accepted'])"
 done
