@@ -107,7 +107,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // row block per workgroup the load -> FFT -> LDS tile -> store chain of the
 // two co-resident workgroups ran nearly serial.
 template <int R>
-constexpr int rowfwd_iters() { return R == 32 ? 4 : 1; }
+constexpr int rowfwd_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }   // N = 256: 2 (r03,
+// with nt A stores: 0.0634 -> 0.0585 ms; 4 row blocks 0.0611)
 
 template <int R, int NT, int SK>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
@@ -407,7 +408,10 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
     const float2 lo = store_round<SK>(lo_r[(32 / TL) * 16 * i]);
     const float2 hi = store_round<SK>(hi_r[(32 / TL) * 16 * i]);
     const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
-    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, 0);
+    // non-temporal (nt): B streams out without taking Infinity-Cache residency, so its write-back
+    // no longer lands on top of k_rowinv's reads (r03: N = 256 k_col2 0.143 -> 0.128 ms and
+    // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419)
+    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, kBufNT);
   }
 }
 

@@ -54,9 +54,12 @@ __device__ __forceinline__ void buf_st2(float2 v, __amdgpu_buffer_rsrc_t rs, int
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
 
-// The once-touched intermediate streams (A, B) keep the default cache policy:
-// non-temporal loads slowed k_rowinv 1.80 -> 2.21 ms and non-temporal stores
-// k_rowfwd 1.17 -> 1.27 ms.
+// The once-touched intermediate streams: loads keep the default cache policy (non-temporal
+// loads slowed k_rowinv 1.80 -> 2.21 ms, r01); the row spectrum A and the column output B are
+// STORED non-temporal since r03 -- with B in slot tiles and A read by k_col2 right after,
+// default-policy stores left their dirty lines in the Infinity Cache to be written back during
+// the next pass (N = 1024 headline 24.9k -> 25.9k (B) -> 26.1k (A and B) on one box; N = 256
+// k_rowinv 0.140 -> 0.100 ms).  (r01, before the tiles: nt A stores 1.17 -> 1.27 ms.)
 __device__ __forceinline__ float2 buf_ld2s(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
   return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
 }
@@ -64,7 +67,12 @@ __device__ __forceinline__ void buf_st2s(float2 v, __amdgpu_buffer_rsrc_t rs, in
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
 }
 __device__ __forceinline__ float4 ld_stream4(const float2* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st_stream4(float2* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st_stream4(float2* p, float4 v) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+}
+// cache-policy bit of buffer instructions (gfx950 aux operand): nt = non-temporal
+constexpr int kBufNT = 2;
 
 // Workgroups b, b+8, b+16, ... land on the same XCD (round-robin dispatch over
 // the 8 XCDs; placement is a speed hint only, never relied on for
