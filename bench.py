@@ -50,6 +50,7 @@ def parse():
                     help="world 1: no process group (by default one is built and the RCCL metric gather runs)")
     ap.add_argument("--no-psf", action="store_true", help="skip the incremental-mode measurement")
     ap.add_argument("--psf-steps", type=int, default=200)
+    ap.add_argument("--no-planes", action="store_true", help="skip the plane-cached FFT mode measurement")
     ap.add_argument("--chunk", type=int, default=0,
                     help="jobs per launch sequence (0 = all envs at once)")
     ap.add_argument("--dbs-flips", type=int, default=65536,
@@ -82,6 +83,15 @@ def algorithmic_bytes(N: int, P: int):
             "k_rowinv": P * N * N * 8 + N * N * 4,
             "k_psf_eval": 16 * N * N,
             "k_psf_commit": 24 * N * N}
+
+
+def plane_cached_bytes(N: int, P: int):
+    """HBM bytes per job of the plane-cached FFT mode (ABI v9): the flipped plane's PAIR runs
+    k_rowfwd / k_col (2 of the P planes), k_rowinv reads the pair's B planes, the P - 2 cached
+    |U_q|^2 planes (f32) and the target channel and writes the pair's fresh |U|^2."""
+    return {"k_rowfwd": 2 * N * N // 8 + 2 * N * N * 4,
+            "k_col": 2 * N * N * 4 + 2 * N * N * 8,
+            "k_rowinv": 2 * N * N * 8 + (P - 2) * N * N * 4 + N * N * 4 + 2 * N * N * 4}
 
 
 def canonical_step_bytes(N: int, P: int) -> int:
@@ -635,6 +645,28 @@ def main():
                 "note": "same env semantics; a flip adds +-h_g(shifted) to the touched plane's cached field "
                         "(linearity of the propagation), no FFT per step; reported separately per SURVEY 8d"}
         vec.close()
+
+    if not args.no_planes and N in (256, 1024):
+        # plane-cached FFT mode: every result the FFT mode's bit for bit (tests/test_gpu_planes.py),
+        # only the flipped plane's pair propagated per step
+        psteps = 4 * args.steps
+        vec, dt, timing, acc_rate = measure("planes", psteps, args.warmup)
+        vec.close()
+        if rank == 0:
+            ps = pass_table(timing, plane_cached_bytes(N, P))
+            step_b = sum(plane_cached_bytes(N, P).values()) * B
+            pms = dt / psteps * 1e3
+            out["plane_cached_mode"] = {
+                "value": round(B * world * psteps / dt, 2), "unit": "env-steps/s", "steps": psteps,
+                "ms_per_step": round(pms, 4), "accept_rate": round(acc_rate, 4),
+                "vs_fft_mode": round((B * world * psteps / dt) / value, 3),
+                "passes": rounded(ps),
+                "step_alg_GBs": round(step_b / (pms * 1e-3) / 1e9, 1),
+                "note": "same env semantics and the FFT mode's results bit for bit: a step propagates only "
+                        "the flipped plane's pair and sums the other planes' cached |U|^2 in the FFT mode's "
+                        "plane order (include/hbx.h ABI v9); reported separately, the headline stays the "
+                        "literal re-propagation of the whole group"}
+        torch.cuda.empty_cache()
 
     if world == 1 and not args.no_ppo:
         # SURVEY 3.2 / BASELINE cfg 4's per-GPU shard: train-PPO.py's env (env.py, 256x256x8 mono),

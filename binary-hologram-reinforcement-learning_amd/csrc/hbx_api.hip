@@ -336,6 +336,7 @@ EnvDev env_dev(const hbx_env_buffers_t* e) {
   d.imp_count = e->imp_count;
   d.state_bytes = e->state_bytes;
   d.recon_pending = e->recon_pending;
+  d.plane_slot = (e->plane_inten && e->plane_slot) ? e->plane_slot : nullptr;
   return d;
 }
 
@@ -357,6 +358,7 @@ EnvDev env_offset(const EnvDev& d, size_t e0, int CH, int G, int N) {
   o.t_psnr_diff = d.t_psnr_diff ? d.t_psnr_diff + e0 : nullptr;
   o.state_bytes = d.state_bytes ? d.state_bytes + e0 * (size_t)CH * N * N : nullptr;
   o.recon_pending = d.recon_pending ? d.recon_pending + e0 : nullptr;
+  o.plane_slot = d.plane_slot ? d.plane_slot + e0 * (size_t)(CH + 2) : nullptr;
   return o;
 }
 
@@ -370,8 +372,13 @@ int check_obs_buffers(const hbx_env_buffers_t* e) {
 // full propagation of n_ids envs (absolute ids from env_ids, or 0..n_ids-1)
 int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, const int32_t* env_ids,
                    int n_ids, float* intensity, double* chan_stats, double* psnr, const EnvDev* env,
-                   float2* field, hipStream_t st) {
+                   float2* field, hipStream_t st, float* plane_pool = nullptr, int32_t* plane_slot = nullptr) {
   const PlanDev& pd = p->pd;
+  const int CHs = pd.G * pd.P + 2;   // plane-cache slots per env
+  if (plane_pool) {                  // identity slots, then every plane's |U|^2 into its slot
+    if (pd.R != 32 && pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+    HBX_HIP(hbx::launch_plane_slot_init(env_ids, n_ids, plane_slot, pd.G * pd.P, st));
+  }
   const int G = pd.G;
   const int chunk = p->max_jobs / G;
   if (intensity) {
@@ -389,7 +396,13 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
     const uint64_t* m = env_ids ? mask : mask + (size_t)i0 * mwords;
     const float* tg = (env_ids || !target) ? target : target + (size_t)i0 * G * pd.N * pd.N;
     float2* fo = field ? (env_ids ? field : field + (size_t)i0 * G * pd.P * pd.N * pd.N) : nullptr;
-    HBX_HIP(hbx::run_jobs(pd, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
+    PlanDev pdx = pd;
+    if (plane_pool) {
+      pdx.plane_mode = hbx::kPlanesFill;
+      pdx.plane_pool = env_ids ? plane_pool : plane_pool + (size_t)i0 * CHs * pd.N * pd.N;
+      pdx.plane_slot = env_ids ? plane_slot : plane_slot + (size_t)i0 * CHs;
+    }
+    HBX_HIP(hbx::run_jobs(pdx, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
                           intensity ? p->job_inten : nullptr, fo, st));
     double* cs = (env_ids || !chan_stats) ? chan_stats : chan_stats + (size_t)i0 * G * 3;
     double* ps = psnr ? (env_ids ? psnr : psnr + i0) : nullptr;
@@ -467,8 +480,13 @@ int hbx_env_reset(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const
   rc = check_obs_buffers(e);
   if (rc) return rc;
   EnvDev ed = env_dev(e);
+  const bool planes = e->plane_inten && e->plane_slot;
+  if ((e->plane_inten != nullptr) != (e->plane_slot != nullptr))
+    return fail(HBX_ERR_INVALID, "plane cache: give both plane_inten and plane_slot");
+  if (planes && e->field) return fail(HBX_ERR_INVALID, "plane cache and env.field (incremental mode) are exclusive");
   rc = propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, &ed,
-                      reinterpret_cast<float2*>(e->field), st);
+                      reinterpret_cast<float2*>(e->field), st, planes ? e->plane_inten : nullptr,
+                      planes ? e->plane_slot : nullptr);
   if (rc) return rc;
   HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, e->state_bytes, e->intensity, e->recon, e->recon_pending,
                                CH, pd.G, (size_t)pd.N * pd.N, st));
@@ -500,6 +518,16 @@ int hbx_field_refresh(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, c
                       int32_t n_ids, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
+  const bool planes = e && e->plane_inten && e->plane_slot && !e->field;
+  if (planes) {   // ABI v9: rebuild the plane cache (and chan_stats / intensity) of the listed envs
+    if (!e->mask || !e->target || !e->chan_stats)
+      return fail(HBX_ERR_INVALID, "plane-cache refresh needs mask, target and chan_stats");
+    const int n = env_ids ? n_ids : n_env;
+    if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_env");
+    HBX_HIP(hipSetDevice(p->device));
+    return propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, e->chan_stats, nullptr, nullptr,
+                          nullptr, (hipStream_t)stream, e->plane_inten, e->plane_slot);
+  }
   if (!e || !e->mask || !e->target || !e->chan_stats || !e->intensity || !e->field)
     return fail(HBX_ERR_INVALID, "refresh needs mask, target, chan_stats, intensity and field");
   const int n = env_ids ? n_ids : n_env;
@@ -540,7 +568,8 @@ int hbx_env_step_psf(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_par
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
   ep.accept_rule = prm->accept_rule;
   ep.reward_kind = prm->reward_kind;
-  const EnvDev base = env_dev(e);
+  EnvDev base = env_dev(e);
+  base.plane_slot = nullptr;   // the incremental step leaves a plane cache alone (the modes are exclusive)
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
     const EnvDev ed = env_offset(base, b0, CH, G, N);
@@ -594,6 +623,11 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   }
   PlanDev pdx = p->pd;            // with recon, k_rowinv writes the stepped group straight into it
   pdx.inten_by_env = to_recon ? 1 : 0;
+  if ((e->plane_inten != nullptr) != (e->plane_slot != nullptr))
+    return fail(HBX_ERR_INVALID, "plane cache: give both plane_inten and plane_slot");
+  const bool planes = e->plane_inten != nullptr;
+  if (planes && pd.R != 32 && pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (planes) pdx.plane_mode = hbx::kPlanesStep;
   EnvParams ep;
   ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
@@ -604,6 +638,10 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     const int n = std::min(p->max_jobs, n_env - b0);
     const EnvDev ed = env_offset(base, b0, CH, G, N);
     float* rec = to_recon ? e->recon + (size_t)b0 * G * hw : nullptr;
+    if (planes) {
+      pdx.plane_pool = e->plane_inten + (size_t)b0 * (CH + 2) * hw;
+      pdx.plane_slot = e->plane_slot + (size_t)b0 * (CH + 2);
+    }
     if (to_recon)   // the previous step's group: recon and intensity agree again before it is overwritten
       HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));

@@ -132,7 +132,18 @@ struct PlanDev {
   int inten_by_env;    // intensity output rows: 0 = job-major [job][N][N]; 1 = env-major
                        // [env][G][N][N] at (job.env, job.group) (the obs recon buffer, ABI v8)
   PassTimer* timer;    // nullable
+  // plane-cached FFT mode (ABI v9; N = 1024 / 256), set per call on a copy of the plan's PlanDev:
+  //   kPlanesOff    no plane cache
+  //   kPlanesFill   full propagation: every plane's |U_p|^2 also goes to its pool slot
+  //   kPlanesStep   env step: only the flipped plane's pair is propagated, the other planes'
+  //                 |U_q|^2 come from the pool (k_rowinv_d sums them in the same plane order,
+  //                 so the group intensity is the FFT mode's bit for bit); the pair's fresh
+  //                 |U|^2 go to the env's two spare slots (swapped in on accept)
+  int plane_mode;
+  float* plane_pool;         // [env][CH + 2][N][N] f32 per-plane |U|^2 (env ids as the jobs carry them)
+  const int32_t* plane_slot; // [env][CH + 2] pool slot of every plane; [CH], [CH + 1] = the spares
 };
+constexpr int kPlanesOff = 0, kPlanesFill = 1, kPlanesStep = 2;
 
 constexpr int kPsfBlocks = 128;   // blocks per job of the incremental-field kernels
                                   // (measured 128 > 256 > 64 > 32, profiles/r01_psf_blocks_ab.txt)
@@ -154,6 +165,8 @@ struct EnvDev {
   int imp_count;
   int8_t* state_bytes;        // [B][CH][H][W] obs["state"] mirror of the mask bits (nullable, ABI v8)
   int32_t* recon_pending;     // [B] group the next step reconciles (nullable; with recon)
+  int32_t* plane_slot;        // [B][CH + 2] plane-cache slots (nullable, ABI v9): an accepted step
+                              // swaps the flipped pair's slots with the two spares
 };
 
 struct EnvParams {
@@ -271,6 +284,8 @@ hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, dou
 // intensity (recon_pending), and rebuild state_bytes / recon of listed envs
 hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
                                   size_t hw, hipStream_t st);
+// plane cache (ABI v9): slot[env][i] = i for the listed envs (env_ids nullable: 0 .. n_ids - 1)
+hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CH, hipStream_t st);
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
                            const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
                            hipStream_t st);

@@ -205,6 +205,16 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     if (env.state_bytes)                                 // obs["state"] mirror (env.py:177 hands out self.state)
       env.state_bytes[((size_t)b * CH + ch) * (size_t)H * W + jb.flip_pix] = (int8_t)((nw >> ((jb.flip_pix % W) & 63)) & 1ull);
     st[3 * g] = js[0]; st[3 * g + 1] = js[1]; st[3 * g + 2] = js[2];
+    if (env.plane_slot) {   // plane cache: the flipped pair's fresh |U|^2 (in the spares) become current
+      int32_t* s = env.plane_slot + (size_t)b * (CH + 2);
+      const int pa = g * P + (jb.flip_plane & ~1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int32_t cur = s[pa + i];
+        s[pa + i] = s[CH + i];
+        s[CH + i] = cur;
+      }
+    }
     env.max_psnr_diff[b] = fmax(env.max_psnr_diff[b], diff);     // env.py:198
     const double sr = (double)flips / (double)steps;              // env.py:200
     env.prev_psnr[b] = psnr_after;                                // env.py:214
@@ -518,6 +528,23 @@ hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* i
   hipLaunchKernelGGL(k_recon_reconcile, dim3(32, n), dim3(256), 0, st, pending, recon, intensity, G, hw);
   return hipGetLastError();
 }
+// plane cache (ABI v9): identity slots of the listed envs (the fill pass writes plane i to slot i,
+// the spares are slots CH and CH + 1)
+__global__ void k_plane_slot_init(const int32_t* __restrict__ env_ids, int n_ids, int32_t* __restrict__ slot,
+                                  int CH) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ids * (CH + 2)) return;
+  const int k = i / (CH + 2), c = i % (CH + 2);
+  const int e = env_ids ? env_ids[k] : k;
+  slot[(size_t)e * (CH + 2) + c] = c;
+}
+
+hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CH, hipStream_t st) {
+  const int n = n_ids * (CH + 2);
+  hipLaunchKernelGGL(k_plane_slot_init, dim3((n + 255) / 256), dim3(256), 0, st, env_ids, n_ids, slot, CH);
+  return hipGetLastError();
+}
+
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
                            const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
                            hipStream_t st) {

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
                                                    const uint32_t* __restrict__ mask,
                                                    float2* __restrict__ ws_a,
                                                    const float2* __restrict__ tw_glob, int P,
-                                                   int CH, float va, float vb) {
+                                                   int CH, float va, float vb, int pair_step) {
   constexpr int N = R * R;
   constexpr int GPB = NT / R;          // rows per row block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
@@ -135,10 +135,11 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   int bid = RIT == 1 ? xcd_pair<RB>(blockIdx.x) : (int)blockIdx.x;
   const int rbw = bid % RBW;
   bid /= RBW;
-  const int q = bid % (P / 2);
-  const int j = bid / (P / 2);
+  const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
+  const int j = bid / npair;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;  // uniform per block
+  const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
   const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
   uint32_t wa[WPR], wb[WPR];
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
                                                      const uint32_t* __restrict__ mask,
                                                      float2* __restrict__ ws_a,
                                                      const float2* __restrict__ tw_glob, int P, int CH,
-                                                     float va, float vb) {
+                                                     float va, float vb, int pair_step) {
   constexpr int R = 32, NT = 256, N = R * R;
   constexpr int GPB = NT / R;          // 8 rows per row block
   constexpr int WPR = N / 32;          // 32 mask words per row = one per lane
@@ -265,10 +266,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
   int bid = RIT == 1 ? xcd_pair<RB>(blockIdx.x) : (int)blockIdx.x;
   const int rbw = bid % RBW;
   bid /= RBW;
-  const int q = bid % (P / 2);
-  const int j = bid / (P / 2);
+  const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
+  const int j = bid / npair;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;  // uniform per block
+  const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
   const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
   uint32_t wa, wb;
@@ -385,14 +387,15 @@ __device__ __forceinline__ float2* col2_region(float2* scratch, int g) {
   return scratch + g * col2_region_stride<R>() + (g >> 1) * (64 / (256 / R));
 }
 
-template <int R>
+template <int R, int SK>
 __device__ __forceinline__ void col2_stage_write(const float2 (&v)[R], float sy, float2* scratch, int grp, int t) {
   float2* reg = col2_region<R>(scratch, grp);
 #pragma unroll
-  for (int k2 = 0; k2 < R; ++k2) reg[R * k2 + t] = make_float2(v[k2].x, sy * v[k2].y);   // row y = t + R k2
+  for (int k2 = 0; k2 < R; ++k2)   // row y = t + R k2
+    reg[R * k2 + t] = store_round<SK>(make_float2(v[k2].x, sy * v[k2].y));
 }
 
-template <int R, int SK>
+template <int R>
 __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
   constexpr int N = R * R, TL = 256 / R, CH = N * TL / 2;   // 16-B chunks per line set
   // chunk c = tid + 256 i: band c / (8 TL) = tid / (8 TL) + (32 / TL) i, row (tid / (TL / 2)) % 16,
@@ -405,8 +408,8 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
   const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
 #pragma unroll
   for (int i = 0; i < CH / 256; ++i) {
-    const float2 lo = store_round<SK>(lo_r[(32 / TL) * 16 * i]);
-    const float2 hi = store_round<SK>(hi_r[(32 / TL) * 16 * i]);
+    const float2 lo = lo_r[(32 / TL) * 16 * i];   // (rounded by col2_stage_write under SK)
+    const float2 hi = hi_r[(32 / TL) * 16 * i];
     const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
     // non-temporal (nt): B streams out without taking Infinity-Cache residency, so its write-back
     // no longer lands on top of k_rowinv's reads (r03: N = 256 k_col2 0.143 -> 0.128 ms and
@@ -420,7 +423,8 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
                                                  const float2* __restrict__ ws_a,
                                                  float2* __restrict__ ws_b,
                                                  const float2* __restrict__ htab,
-                                                 const float2* __restrict__ tw_glob, int P) {
+                                                 const float2* __restrict__ tw_glob, int P,
+                                                 int pair_step) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // lane groups (= input lines) per block iteration
   constexpr int ITER = col2_iters<R>();
@@ -438,10 +442,11 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   int bid = blockIdx.x;
   const int lb = bid % LB;
   bid /= LB;
-  const int p = bid % P;
-  const int j = bid / P;
+  const int np = pair_step ? 2 : P;     // plane-cached step: the flipped plane's pair only
+  const int j = bid / np;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;
+  const int p = pair_step ? (jb.flip_plane & ~1) + bid % 2 : bid % np;
   using PA = LayoutA<R>;   // A planes: N/2 lines
   using PB = LayoutB<R>;   // B planes: N lines
   const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * plane_a_elems(R), plane_a_elems(R) * 8);
@@ -523,9 +528,9 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
     const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(W)
     if constexpr (kTiledB<R>) {
       const int kxb = kx - grp;            // the block's GPB lines: slot tile kxb / GPB
-      col2_stage_write<R>(v, 1.0f, scratch, grp, t);
+      col2_stage_write<R, SK>(v, 1.0f, scratch, grp, t);
       lds_barrier();
-      col2_stage_store<R, SK>(scratch, rb, kxb / GPB);
+      col2_stage_store<R>(scratch, rb, kxb / GPB);
       if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
         const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
@@ -534,9 +539,9 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       fft_group_s1<R, true, true>(w, t, tw);
       lds_barrier();   // the first set has been read out: the regions are the FFTs' again
       fft_group_s2<R, true, true>(w, t, sc);
-      col2_stage_write<R>(w, sy, scratch, grp, t);
+      col2_stage_write<R, SK>(w, sy, scratch, grp, t);
       lds_barrier();
-      col2_stage_store<R, SK>(scratch, rb, (N / 2 + kxb) / GPB);
+      col2_stage_store<R>(scratch, rb, (N / 2 + kxb) / GPB);
     } else {
       {
         const int vo = PB::voff(t, kx);
@@ -623,7 +628,9 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
                                                      const float* __restrict__ target,
                                                      const float2* __restrict__ tw_glob, int P, int G,
                                                      double* __restrict__ partial, float* __restrict__ inten_out,
-                                                     float2* __restrict__ field_out, size_t tmask, int inten_by_env) {
+                                                     float2* __restrict__ field_out, size_t tmask, int inten_by_env,
+                                                     int plane_mode, float* __restrict__ plane_pool,
+                                                     const int32_t* __restrict__ plane_slot) {
   constexpr int N = R * R, GPB = 256 / R, RB = N / GPB, TL = 256 / R;
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
@@ -670,17 +677,57 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
 #pragma unroll
   for (int k = 0; k < R; ++k) acc[k] = 0.0f;
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
+  // plane cache (ABI v9): slots of this env's planes, pool rows of this lane group's row y
+  const int CH = G * P;
+  const int32_t* slots = plane_slot ? plane_slot + (size_t)jb.env * (CH + 2) : nullptr;
+  auto pool_row = [&](int slot) { return plane_pool + (((size_t)jb.env * (CH + 2) + slot) * N + y) * N; };
   auto finish_plane = [&](pk2 (&v)[R], int p) {
     fft_group<R, true>(v, t, sc, tw);
+    float f[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+    for (int k = 0; k < R; ++k) {
+      f[k] = fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+      acc[k] += f[k];
+    }
     if (field_out) {  // exact field of this plane (incremental mode init / refresh)
       float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * N + y) * N;
 #pragma unroll
       for (int k = 0; k < R; ++k) frow[t + R * k] = from_pk(v[k]);
     }
+    // |U_p|^2 to the plane cache: every plane on a fill; on a step both planes of the flipped pair
+    // go to the two spares -- the partner's bits change too (the pair is ONE complex row FFT, so
+    // its rounding sees the flipped plane), which is why a step keeps both
+    if (plane_mode != kPlanesOff) {
+      float* orow = pool_row(slots[plane_mode == kPlanesFill ? jb.group * P + p : CH + (p & 1)]);
+#pragma unroll
+      for (int k = 0; k < R; ++k) __builtin_nontemporal_store(f[k], orow + t + R * k);
+    }
+  };
+  // a cached plane's |U_q|^2 added in its place in the plane order (the sum is the FFT mode's
+  // sum bit for bit: acc = ((0 + c_0) + c_1) + ..., each c_q the same f32 value)
+  auto add_cached = [&](int q) {
+    const float* crow = pool_row(slots[jb.group * P + q]);
+    float c[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) c[k] = __builtin_nontemporal_load(crow + t + R * k);
+#pragma unroll
+    for (int k = 0; k < R; ++k) acc[k] += c[k];
   };
   pk2 va[R];
+  if (plane_mode == kPlanesStep) {   // only the flipped plane's pair is in B
+    const int pa = jb.flip_plane & ~1;
+    load_plane(va, pa);
+    __syncthreads();  // tw visible
+#pragma unroll 1
+    for (int q = 0; q < pa; ++q) add_cached(q);
+    finish_plane(va, pa);
+    load_plane(va, pa + 1);
+    finish_plane(va, pa + 1);
+#pragma unroll 1
+    for (int q = pa + 2; q < P; ++q) add_cached(q);
+    rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
+    return;
+  }
   load_plane(va, 0);
   __syncthreads();  // tw visible
   if constexpr (R == 16) {   // N = 256: registers to spare -- the next plane in flight under this one's FFT
@@ -935,22 +982,25 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   const int P = pd.P;
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
+  const int pair = pd.plane_mode == kPlanesStep ? 1 : 0;
+  if (pd.plane_mode != kPlanesOff && (!kTiledB<R> || !pd.plane_pool || !pd.plane_slot)) return hipErrorInvalidValue;
   {
-    const unsigned blocks = (unsigned)n_jobs * (P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
+    const unsigned blocks = (unsigned)n_jobs * (pair ? 1 : P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
     if (tm) tm->begin(0, st);
     if constexpr (R == 32)
       hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
-                         pd.va, pd.vb);
+                         pd.va, pd.vb, pair);
     else
     hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
-                       CH, pd.va, pd.vb);
+                       CH, pd.va, pd.vb, pair);
     if (tm) tm->end(0, n_jobs, st);
   }
   {
     if (tm) tm->begin(1, st);
     constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
-    const unsigned blocks = (unsigned)n_jobs * P * ((N / 2) / LINES_PER_BLOCK);
-    hipLaunchKernelGGL((k_col2<R, SK>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P);
+    const unsigned blocks = (unsigned)n_jobs * (pair ? 2 : P) * ((N / 2) / LINES_PER_BLOCK);
+    hipLaunchKernelGGL((k_col2<R, SK>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P,
+                       pair);
     if (tm) tm->end(1, n_jobs, st);
   }
   {
@@ -959,7 +1009,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if constexpr (kTiledB<R>)
       hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
                          pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
-                         pd.inten_by_env);
+                         pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot);
     else
       hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                          target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,

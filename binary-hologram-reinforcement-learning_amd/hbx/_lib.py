@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 8
+ABI_VERSION = 9
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -82,6 +82,7 @@ class EnvBuffers(C.Structure):
         ("imp_changes", C.c_void_p), ("imp_values", C.c_void_p), ("t_psnr_diff", C.c_void_p),
         ("imp_count", C.c_int32), ("reserved", C.c_int32),
         ("state_bytes", C.c_void_p), ("recon", C.c_void_p), ("recon_pending", C.c_void_p),
+        ("plane_inten", C.c_void_p), ("plane_slot", C.c_void_p),   # ABI v9 plane cache
     ]
 
 

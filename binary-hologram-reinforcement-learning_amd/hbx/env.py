@@ -83,7 +83,7 @@ class EnvState:
 
     def __init__(self, plan: Plan, n_env: int, keep_record: bool = True, keep_pre_model: bool = True,
                  keep_intensity: bool = True, keep_field: bool = False, importance_samples: int = 0,
-                 keep_state_bytes: bool = False, keep_recon: bool = False):
+                 keep_state_bytes: bool = False, keep_recon: bool = False, keep_planes: bool = False):
         c, dev = plan.cfg, plan.device
         self.plan, self.n = plan, n_env
         keep_intensity = keep_intensity or keep_field or keep_recon   # the incremental mode / recon need it
@@ -97,6 +97,12 @@ class EnvState:
         # complex64 field of every plane, as float32 pairs (incremental-field mode)
         self.field = torch.zeros((n_env, c.channels, c.height, c.width, 2), dtype=torch.float32,
                                  device=dev) if keep_field else None
+        # plane-cached FFT mode (ABI v9): |U_p|^2 of every plane plus two spare slots per env, and
+        # the slot table (reset fills both; an accepted step swaps the flipped pair with the spares)
+        self.plane_inten = torch.empty((n_env, c.channels + 2, c.height, c.width), dtype=torch.float32,
+                                       device=dev) if keep_planes else None
+        self.plane_slot = torch.zeros((n_env, c.channels + 2), dtype=torch.int32,
+                                      device=dev) if keep_planes else None
         self.mask = torch.zeros(plan.mask_shape(n_env), dtype=torch.int64, device=dev)
         self.record = torch.zeros((n_env, c.channels, c.height, c.width), dtype=torch.int8,
                                   device=dev) if keep_record else None
@@ -131,6 +137,7 @@ class EnvState:
         b.imp_changes, b.imp_values, b.t_psnr_diff = p(self.imp_changes), p(self.imp_values), p(self.t_psnr_diff)
         b.imp_count = k
         b.state_bytes, b.recon, b.recon_pending = p(self.state_bytes), p(self.recon), p(self.recon_pending)
+        b.plane_inten, b.plane_slot = p(self.plane_inten), p(self.plane_slot)
 
     def check_error(self):
         if int(self.error.item()) != 0:
@@ -167,6 +174,9 @@ class HologramVecEnv(_VecEnvBase):
     (include/hbx.h hbx_env_step_psf): same results within fp32 tolerance, one
     streaming pass over the touched plane's cached field instead of 2-D FFTs;
     the cached fields are re-propagated exactly every ``refresh_every`` steps.
+    mode="planes" is the plane-cached FFT mode (ABI v9): every result bit for bit
+    the FFT mode's, but a step propagates only the flipped plane's pair and sums
+    the other planes' cached |U|^2 (4 B/px per plane kept per env).
     """
 
     def __init__(self, cfg: OpticsConfig, num_envs: int, target_source: Callable,
@@ -180,8 +190,10 @@ class HologramVecEnv(_VecEnvBase):
                  action_format: str = "discrete", obs_format: str = "torch"):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
-        if mode not in ("fft", "psf"):
-            raise ValueError(f"mode must be 'fft' or 'psf', got {mode!r}")
+        if mode not in ("fft", "psf", "planes"):
+            raise ValueError(f"mode must be 'fft', 'psf' or 'planes', got {mode!r}")
+        if mode == "planes" and cfg.height not in (256, 1024):
+            raise ValueError("mode='planes' is built for N = 256 and 1024")
         if mode == "psf" and "recon_image" in obs_keys:
             raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
                              "drop it from obs_keys or use mode='fft'")
@@ -215,7 +227,8 @@ class HologramVecEnv(_VecEnvBase):
                               keep_field=(mode == "psf"),
                               importance_samples=self.importance_samples,
                               keep_state_bytes="state" in self.obs_keys,
-                              keep_recon="recon_image" in self.obs_keys)
+                              keep_recon="recon_image" in self.obs_keys,
+                              keep_planes=(mode == "planes"))
         self.target_source = target_source
         self.pre_model_fn = pre_model_fn
         self.pre_model_source = pre_model_source
@@ -377,8 +390,9 @@ class HologramVecEnv(_VecEnvBase):
         return out
 
     def refresh(self):
-        """Exact FFT re-propagation of the cached fields (incremental mode)."""
-        if self.mode == "psf":
+        """Exact FFT re-propagation of the cached fields (incremental mode) or of the
+        plane cache (plane-cached mode; needed only after restoring masks)."""
+        if self.mode in ("psf", "planes"):
             self.plan.field_refresh(self.state.bufs, self.num_envs)
             self._since_refresh = 0
 
@@ -557,7 +571,7 @@ class HologramVecEnv(_VecEnvBase):
                 t = getattr(st, k)
                 if t is not None and k in z.files:
                     t.copy_(torch.from_numpy(z[k]))
-        if self.mode == "psf":
+        if self.mode in ("psf", "planes"):
             self.refresh()
         # obs["state"] follows the restored mask; recon from the intensity cache when the
         # snapshot holds no recon of its own

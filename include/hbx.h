@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 8
+#define HBX_ABI_VERSION 9
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -121,6 +121,22 @@ typedef struct hbx_env_buffers {
                               intensity -> recon; 0: none).  With recon given,
                               env->intensity of the last stepped group is
                               current only after that reconcile.             */
+  /* ABI v9: plane-cached FFT mode (N = 1024 / 256; both non-null, with
+   * hbx_env_reset / hbx_field_refresh filling them).  A step changes ONE plane
+   * of the touched group, and the FFT mode's re-propagation of the other plane
+   * pairs reproduces their |U_q|^2 bit for bit (deterministic kernels), so the
+   * step propagates only the flipped plane's pair and sums the cached planes
+   * in the same plane order: the group intensity, statistics, PSNR, reward and
+   * every decision are the FFT mode's bit for bit (env.py:170-174 work, 1/4 of
+   * the propagation).  The pair is propagated, not the flipped plane alone:
+   * k_rowfwd transforms two planes as the real and imaginary parts of one
+   * complex FFT, so the partner's rounding sees the flipped plane and its bits
+   * change too.  Both fresh |U|^2 go to the env's two spare slots and are
+   * swapped in on accept (rollback: nothing to undo). */
+  float* plane_inten;      /* [B][G*P + 2][H][W] f32 pool of per-plane |U|^2  */
+  int32_t* plane_slot;     /* [B][G*P + 2] pool slot of each plane; [G*P] and
+                              [G*P + 1] are the spares (caller-owned, filled
+                              by reset)                                       */
 } hbx_env_buffers_t;
 
 /* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
@@ -357,7 +373,9 @@ int hbx_env_obs_sync(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_en
 
 /* Exact re-propagation (FFT path) of env->field, env->intensity and
  * env->chan_stats for the listed envs (bounds the fp32 drift of the
- * incremental updates; counters and PSNR history are left untouched). */
+ * incremental updates; counters and PSNR history are left untouched).
+ * ABI v9: with env->plane_inten / plane_slot (and no field) it rebuilds the
+ * plane cache instead (after a checkpoint load). */
 int hbx_field_refresh(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
                       const int32_t* env_ids, int32_t n_ids, void* stream);
 

@@ -1,0 +1,113 @@
+"""Plane-cached FFT mode (ABI v9, HologramVecEnv(mode="planes")).
+
+A step of env.py:154-259 flips ONE pixel of one plane; the FFT mode re-propagates all P planes of
+the touched colour group, and the P - 1 untouched planes' |U_q|^2 come out bit-identical every
+time (deterministic kernels, same inputs).  The plane-cached mode keeps each plane's |U_q|^2,
+propagates only the flipped plane's pair (the pair packing of k_rowfwd is kept, so the two planes'
+values are the FFT mode's bits too) and sums the planes in the same order.  So the claim tested
+here is bit-exactness against the FFT mode, step by step, with rollbacks and resets:
+rewards, PSNRs, accept / terminate / truncate flags, masks, records, channel statistics and the
+recon_image observation.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _pair(cfg, B, seed, max_steps=10000, obs_keys=None):
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    pres = [torch.rand((cfg.channels, cfg.height, cfg.width), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, cfg.height, cfg.width), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=max_steps,
+              obs_keys=OBS_KEYS if obs_keys is None else obs_keys)
+    fft = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="fft", **kw)
+    planes = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="planes", **kw)
+    return fft, planes, g
+
+
+def _same_state(a, b, what):
+    sa, sb = a.state, b.state
+    for k in ("mask", "record", "chan_stats", "prev_psnr", "init_psnr", "steps", "flip_count", "sustained"):
+        assert torch.equal(getattr(sa, k), getattr(sb, k)), (what, k)
+
+
+@pytest.mark.parametrize("N,B,steps,max_steps", [(1024, 4, 120, 10000), (256, 16, 300, 40)])
+def test_planes_mode_bit_exact_vs_fft_mode(N, B, steps, max_steps):
+    import hbx
+    cfg = hbx.rgb_config(1024) if N == 1024 else hbx.mono_config(256)
+    fft, planes, g = _pair(cfg, B, 5 + N, max_steps=max_steps)
+    o1, o2 = fft.reset(), planes.reset()
+    assert torch.equal(o1["recon_image"], o2["recon_image"])
+    _same_state(fft, planes, "reset")
+    acts = torch.randint(0, cfg.channels * N * N, (steps, B), generator=g, device="cuda")
+    n_acc = n_rej = n_done = 0
+    for k in range(steps):
+        o1, r1, d1, _ = fft.step(acts[k])
+        o2, r2, d2, _ = planes.step(acts[k])
+        assert np.array_equal(r1, r2), k
+        assert np.array_equal(d1, d2), k
+        assert torch.equal(fft._psnr, planes._psnr), k
+        assert torch.equal(fft._acc, planes._acc), k
+        assert torch.equal(o1["recon_image"], o2["recon_image"]), k      # stepped (pre-rollback) group too
+        assert torch.equal(o1["state"], o2["state"]), k
+        n_acc += int(fft._acc.sum())
+        n_rej += int((1 - fft._acc).sum())
+        n_done += int(np.sum(d1))
+        if k % 30 == 0 or k == steps - 1:
+            _same_state(fft, planes, k)
+    assert n_acc > 0 and n_rej > 0
+    if max_steps < steps:
+        assert n_done > 0          # auto resets of subsets of envs went through the fill pass
+
+
+def test_planes_cache_holds_current_planes_and_resumes(tmp_path):
+    """After random steps every cached plane equals |U_q|^2 of the current mask (hbx_simulate);
+    a save() / load() round trip rebuilds the cache and the env continues bit for bit."""
+    import hbx
+    cfg = hbx.rgb_config(256)
+    B = 3
+    fft, planes, g = _pair(cfg, B, 11)
+    fft.reset()
+    planes.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (80, B), generator=g, device="cuda")
+    for k in range(40):
+        fft.step(acts[k])
+        planes.step(acts[k])
+    st = planes.state
+    field, _ = planes.plan.simulate(st.mask)
+    inten = field.real ** 2 + field.imag ** 2                             # |U|^2 per plane (f32)
+    slots = st.plane_slot.long()
+    for b in range(B):
+        got = st.plane_inten[b][slots[b, :cfg.channels]]
+        assert torch.allclose(got, inten[b], rtol=1e-5, atol=1e-6 * float(inten[b].max()))
+    path = str(tmp_path / "planes.npz")
+    planes.save(path)
+    planes2 = type(planes)(cfg, B, planes.target_source, pre_model_source=planes.pre_model_source,
+                           mode="planes", auto_reset=True)
+    planes2.reset()
+    planes2.load(path)
+    for k in range(40, 80):
+        o1, r1, d1, _ = fft.step(acts[k])
+        o2, r2, d2, _ = planes2.step(acts[k])
+        assert np.array_equal(r1, r2), k
+        assert torch.equal(o1["recon_image"], o2["recon_image"]), k
+    _same_state(fft, planes2, "resumed")
+
+
+def test_planes_mode_rejects_unbuilt_sizes_and_half_buffers():
+    import hbx
+    from hbx.env import HologramVecEnv
+    cfg = hbx.rgb_config(64)
+    with pytest.raises(ValueError):
+        HologramVecEnv(cfg, 2, lambda i: torch.rand(3, 64, 64), pre_model_source=lambda i: torch.rand(24, 64, 64),
+                       mode="planes")
+    cfg = hbx.mono_config(256)
+    env = HologramVecEnv(cfg, 2, lambda i: torch.rand(1, 256, 256, device="cuda"),
+                         pre_model_source=lambda i: torch.rand(8, 256, 256, device="cuda"), mode="planes")
+    env.reset()
+    env.state.bufs.plane_slot = None                                     # pool without slot table
+    with pytest.raises(RuntimeError):
+        env.step_device(torch.zeros(2, dtype=torch.int64, device="cuda"))

@@ -49,6 +49,33 @@ def run(n, k=16):
     print(f"  f32  eval changes {np.round(fps[:6] - f0, 12)}")
 
 
+def determinism(n, prec):
+    """Is a bf16 group propagation a function of its inputs alone?  The same mask twice in
+    one launch, twice in separate launches, and the same flip at several job positions."""
+    cfg = rgb_config(n)
+    rng = np.random.default_rng(0)
+    pre = torch.from_numpy(rng.random((24, n, n), np.float32)).cuda()
+    tgt = torch.from_numpy(rng.random((3, n, n), np.float32)).cuda()
+    mask = pack_bits(pre >= 0.5)
+    plan = Plan(cfg, max_jobs=256, precision=prec)
+    _, s1, _ = plan.propagate(mask.unsqueeze(0), tgt.unsqueeze(0), want_intensity=False)
+    _, s2, _ = plan.propagate(mask.unsqueeze(0), tgt.unsqueeze(0), want_intensity=False)
+    _, s3, _ = plan.propagate(torch.stack([mask, mask, mask]), torch.stack([tgt, tgt, tgt]), want_intensity=False)
+    f = torch.tensor([5 * n * n + 77 * n + 300] * 5, device="cuda")
+    _, g1 = plan.eval_flips(mask, tgt, s1[0].contiguous(), f)
+    print(f"N={n} prec={prec}: launch-to-launch max |d stats| {float((s1 - s2).abs().max()):.3e}; "
+          f"env0/env1/env2 of one launch {float((s3[0] - s3[1]).abs().max()):.3e} "
+          f"{float((s3[0] - s3[2]).abs().max()):.3e}; one env vs three {float((s1[0] - s3[0]).abs().max()):.3e}")
+    print(f"  same flip at 5 job positions: max spread {float((g1 - g1[0]).abs().max()):.3e}; stats {g1[:2].tolist()}")
+    plan.close()
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["det"]:
+        determinism(1024, PRECISION_BF16_STORE)
+        sys.exit(0)
+    for n in (256, 1024):
+        for prec in (PRECISION_F32, PRECISION_BF16_STORE):
+            determinism(n, prec)
     for n in (64, 256, 1024):
         run(n)
