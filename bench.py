@@ -703,6 +703,16 @@ def main():
                     lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12)
             if args.cpu_sample > 0:
                 out["ppo_mono_256"]["cpu_baseline"] = cpu_baseline_mono(max(40, 25 * args.cpu_sample))
+        if not args.no_planes:      # the same mono step in the plane-cached FFT mode (bit-exact)
+            vec, dt, timing, _ = measure("planes", msteps, args.warmup, mcfg=mono)
+            vec.close()
+            if rank == 0:
+                pps = pass_table(timing, plane_cached_bytes(256, mono.planes))
+                out["ppo_mono_256"]["plane_cached_mode"] = {
+                    "value": round(B * msteps / dt, 2), "unit": "env-steps/s",
+                    "ms_per_step": round(dt / msteps * 1e3, 4),
+                    "vs_fft_mode": round((B * msteps / dt) / out["ppo_mono_256"]["value"], 3),
+                    "passes": rounded(pps)}
 
     if rank == 0:
         if world == 1 and args.cpu_sample > 0:
