@@ -367,7 +367,8 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 // Measured and removed: the round-1 LDS mirror, packed DFTs,
 // three workgroups per CU, H issued ahead, B panels of 8 / 32 / 64 rows.
 template <int R>
-// Lines per lane group.  Measured r03: N = 1024 ITER 2 / 4 / 8 = 2.94 / 2.72 / 2.76 ms.  N = 256:
+// Lines per lane group.  Measured r03: N = 1024 ITER 2 / 4 / 8 = 2.94 / 2.72 / 2.76 ms (with the
+// nt B stores, r03i: 2.82 / 2.58-2.60 / 2.68-2.70).  N = 256:
 // ITER 4 = 0.152 ms, 2 = 0.144; ITER 1 timed 0.142 but wrote wrong B rows (193-223, odd, in
 // workgroups >= 256 only; not an uninitialised-LDS read: NaN-filled scratch changes nothing)
 // -- not understood, so not used (profiles/r03/kcol2_iter1_anomaly.txt).
