@@ -365,7 +365,7 @@ def cpu_baseline_mono(n_steps: int, N: int = 256):
                       f"(oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
 
 
-def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed):
+def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=False):
     """The step an SB3 learner calls (train-PPO.py:296-322): HologramVecEnv.step with all
     five observation keys (env.py:176-181) as device tensors, rewards / dones to the host,
     every step.  The observations are views of buffers the step kernels keep current
@@ -374,7 +374,8 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed):
     import torch
     from hbx.env import OBS_KEYS, HologramVecEnv
     vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format="torch",
-                         auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0)
+                         auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0,
+                         graph=graph)
     vec.reset()
     gen = torch.Generator(device="cuda").manual_seed(seed)
     n_pix = mcfg.channels * mcfg.height * mcfg.width
@@ -394,7 +395,7 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed):
     vec.close()
     ms = dt / steps * 1e3
     return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps,
-            "ms_per_step": round(ms, 4), "bare_step_ms": round(bare_ms, 4),
+            "graph": graph, "ms_per_step": round(ms, 4), "bare_step_ms": round(bare_ms, 4),
             "obs_overhead_frac": round(ms / bare_ms - 1.0, 4), "obs_keys": list(obs.keys()),
             "obs_shapes": shapes, "obs_are_views": views,
             "note": "HologramVecEnv.step (SB3 VecEnv surface, obs_format='torch', auto_reset on): all five "
@@ -613,6 +614,9 @@ def main():
         out["vecenv_step_obs"] = vecenv_step_obs(
             cfg, B, args.steps, args.warmup, lambda i: target_source(i), lambda i: pre_model_source(i),
             ms_per_step, 11)
+        out["vecenv_step_obs"]["graph_replay"] = {k: v for k, v in vecenv_step_obs(
+            cfg, B, args.steps, args.warmup, lambda i: target_source(i), lambda i: pre_model_source(i),
+            ms_per_step, 11, graph=True).items() if k in ("value", "ms_per_step", "obs_overhead_frac")}
         torch.cuda.empty_cache()
 
     if rank == 0 and world == 1 and args.dbs_flips > 0:
@@ -701,6 +705,11 @@ def main():
                     mono, B, args.steps, args.warmup,
                     lambda i: target_source(i)[:1, :256, :256].contiguous(),
                     lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12)
+                out["ppo_mono_256"]["vecenv_step_obs"]["graph_replay"] = {k: v for k, v in vecenv_step_obs(
+                    mono, B, 4 * args.steps, args.warmup,
+                    lambda i: target_source(i)[:1, :256, :256].contiguous(),
+                    lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12,
+                    graph=True).items() if k in ("value", "ms_per_step", "obs_overhead_frac")}
             if args.cpu_sample > 0:
                 out["ppo_mono_256"]["cpu_baseline"] = cpu_baseline_mono(max(40, 25 * args.cpu_sample))
         if not args.no_planes:      # the same mono step in the plane-cached FFT mode (bit-exact)

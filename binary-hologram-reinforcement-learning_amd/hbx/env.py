@@ -187,7 +187,7 @@ class HologramVecEnv(_VecEnvBase):
                  device: Optional[int] = None, pre_model_source: Optional[Callable] = None,
                  mode: str = "fft", refresh_every: int = 2048, reward: str = "psnr",
                  importance_samples: int = 10000, importance_seed: int = 0,
-                 action_format: str = "discrete", obs_format: str = "torch"):
+                 action_format: str = "discrete", obs_format: str = "torch", graph: bool = False):
         if (pre_model_fn is None) == (pre_model_source is None):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
         if mode not in ("fft", "psf", "planes"):
@@ -206,6 +206,13 @@ class HologramVecEnv(_VecEnvBase):
         if reward not in ("psnr", "importance"):
             raise ValueError(f"reward must be 'psnr' or 'importance', got {reward!r}")
         self.mode = mode
+        # graph=True: the device step (its ~7 kernel launches) is captured once into a HIP graph
+        # and replayed -- one launch per SB3 step() instead of several, where the per-step host
+        # sync leaves the launch overhead exposed (FFT / plane-cached modes; the default stream
+        # outputs only, i.e. step() / step_device() without out=)
+        self.use_graph = bool(graph) and mode in ("fft", "planes")
+        self._graph = None
+        self._g_actions = None
         self.reward_kind = reward
         self.importance_samples = int(importance_samples) if reward == "importance" else 0
         self.importance_seed = int(importance_seed)
@@ -385,9 +392,33 @@ class HologramVecEnv(_VecEnvBase):
             self._since_refresh += 1
             if self.refresh_every and self._since_refresh >= self.refresh_every:
                 self.refresh()
+        elif self.use_graph and out[0] is self._reward and self.device.type == "cuda":
+            self._graph_step(actions)
         else:
             self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, *out)
         return out
+
+    def _graph_step(self, actions: torch.Tensor):
+        """hbx_env_step replayed from a captured HIP graph (static buffers: the env's own
+        state and output row, a static action vector).  Capture records the launches without
+        running them; the replay right after runs this step."""
+        if self._graph is None:
+            self._g_actions = actions.clone()
+            out = (self._reward, self._psnr, self._acc, self._term, self._trunc)
+            # the step must run once eagerly first: lazy plan buffers are allocated on first use
+            if not getattr(self, "_graph_warm", False):
+                self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, *out)
+                self._graph_warm = True
+                return
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.graph(g, stream=s):
+                self.plan.env_step(self.state.bufs, self.params, self.num_envs, self._g_actions, *out)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._graph = g
+        self._g_actions.copy_(actions)
+        self._graph.replay()
 
     def refresh(self):
         """Exact FFT re-propagation of the cached fields (incremental mode) or of the

@@ -136,3 +136,34 @@ def test_obs_step_matches_oracle_small():
         assert np.array_equal(obs["state"][0, 0].cpu().numpy(), ref.state.astype(np.int8))
     assert saw == {True, False}
     env.close()
+
+
+@pytest.mark.parametrize("mode", ["fft", "planes"])
+def test_graph_replayed_step_equals_eager(mode):
+    """HologramVecEnv(graph=True): the device step captured once into a HIP graph and replayed
+    gives the eager step's rewards, flags, observations and state at every step, across
+    auto-resets of env subsets (which run eagerly between replays)."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.mono_config(256)
+    B = 8
+    g = torch.Generator(device="cuda").manual_seed(23)
+    pres = [torch.rand((cfg.channels, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=25, obs_keys=OBS_KEYS, mode=mode)
+    eager = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    graph = HologramVecEnv(cfg, B, lambda i: tgts[i], graph=True, **kw)
+    eager.reset()
+    graph.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (80, B), generator=g, device="cuda")
+    n_done = 0
+    for k in range(80):
+        o1, r1, d1, _ = eager.step(acts[k])
+        o2, r2, d2, _ = graph.step(acts[k])
+        assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
+        for key in OBS_KEYS:
+            assert torch.equal(o1[key], o2[key]), (k, key)
+        n_done += int(d1.sum())
+    assert graph._graph is not None and n_done > 0
+    for key in ("mask", "chan_stats", "prev_psnr", "steps", "flip_count"):
+        assert torch.equal(getattr(eager.state, key), getattr(graph.state, key)), key
