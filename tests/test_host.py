@@ -215,3 +215,30 @@ def test_walk_k_choice():
     from hbx import _lib
     for q in (0.9, 0.5, 0.3):                          # frequent accepts: one-launch two-accept steps
         assert walk_k(q, 1024) in _lib.WALK_FUSED_K
+
+
+def test_vecenv_mode_validation_before_any_device_work():
+    """mode='planes' is built for N = 256 / 1024 only and graph replay applies to the FFT-type
+    modes: both are decided from the arguments before a plan (or the GPU) is touched."""
+    import pytest
+    import hbx
+    from hbx.env import HologramVecEnv
+    src = lambda i: None  # noqa: E731  (never called: construction fails first)
+    with pytest.raises(ValueError, match="planes"):
+        HologramVecEnv(hbx.rgb_config(64), 2, src, pre_model_source=src, mode="planes")
+    with pytest.raises(ValueError, match="mode must be"):
+        HologramVecEnv(hbx.mono_config(256), 2, src, pre_model_source=src, mode="cached")
+
+
+def test_env_buffers_struct_matches_header():
+    """ctypes mirror of hbx_env_buffers_t (include/hbx.h, ABI v9): field order and offsets."""
+    import ctypes as C
+    import re
+    from hbx import _lib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "include", "hbx.h")).read()
+    body = hdr[hdr.index("typedef struct hbx_env_buffers {"):hdr.index("} hbx_env_buffers_t;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"\b(\w+);", body)
+    assert [f[0] for f in _lib.EnvBuffers._fields_] == names
+    assert C.sizeof(_lib.EnvBuffers) == 8 * (len(names) - 2) + 4 * 2   # two int32 fields
