@@ -142,7 +142,10 @@ def _imread(path: str, gray: bool = False) -> torch.Tensor:
 
 
 class TargetFolder:
-    """Sorted ``*.png`` targets of a directory as (target [1, C, IPS, IPS], path)."""
+    """Sorted ``*.png`` targets of a directory.  ``ds[i]`` is (target [1, C, IPS, IPS], path);
+    iterating yields what ``DataLoader(Dataset512(...), batch_size=1)`` yields, the batched
+    target and the collated name LIST ``[path]`` (``a, imgname = next(iter(trainloader))``,
+    DBS_1024_24.py:271; env.py:96-104 prints it), so it drops in for the reference's loader."""
 
     def __init__(self, target_dir: str, ips: int = 1024, train: bool = True, padding: int = 0,
                  gray: bool = False, seed: Optional[int] = None):
@@ -178,4 +181,5 @@ class TargetFolder:
 
     def __iter__(self):
         for i in range(len(self)):
-            yield self[i]
+            t, path = self[i]
+            yield t, [path]

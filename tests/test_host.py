@@ -183,6 +183,8 @@ def test_target_folder(tmp_path):
     assert t2.shape == (1, 3, 36, 36)
     tr = TargetFolder(str(tmp_path), ips=32, train=True, seed=3)
     assert tr[1][0].shape == (1, 3, 32, 32)
+    a, imgname = next(iter(ds))                      # DataLoader(batch_size=1) shape of a batch
+    assert a.shape == (1, 3, 36, 36) and isinstance(imgname, list) and imgname[0].endswith("a.png")
 
 
 def test_crop_bits_matches_oracle_crop():
