@@ -63,6 +63,30 @@ def test_planes_mode_bit_exact_vs_fft_mode(N, B, steps, max_steps):
         assert n_done > 0          # auto resets of subsets of envs went through the fill pass
 
 
+def test_planes_mode_chunked_launches_equal_fft_mode():
+    """More envs than the plan's max_jobs: the step and the reset fill run in launch chunks, the
+    pool / slot pointers offset per chunk (hbx_env_step, propagate_full) -- still bit-exact."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.mono_config(256)
+    B = 7
+    g = torch.Generator(device="cuda").manual_seed(41)
+    pres = [torch.rand((cfg.channels, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=15, obs_keys=OBS_KEYS, max_jobs=3)
+    fft = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="fft", **kw)
+    planes = HologramVecEnv(cfg, B, lambda i: tgts[i], mode="planes", **kw)
+    fft.reset()
+    planes.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (50, B), generator=g, device="cuda")
+    for k in range(50):
+        o1, r1, d1, _ = fft.step(acts[k])
+        o2, r2, d2, _ = planes.step(acts[k])
+        assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
+        assert torch.equal(o1["recon_image"], o2["recon_image"]), k
+    _same_state(fft, planes, "chunked")
+
+
 def test_planes_cache_holds_current_planes_and_resumes(tmp_path):
     """After random steps every cached plane equals |U_q|^2 of the current mask (hbx_simulate);
     a save() / load() round trip rebuilds the cache and the env continues bit for bit."""

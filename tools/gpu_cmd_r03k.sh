@@ -3,6 +3,8 @@
 # one GPU (gloo, both ranks on cuda:0: a code-path check, not a scaling measurement)
 set -o pipefail
 mkdir -p gpurun_out/r03k
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r03k/smoke.txt 2>&1 || exit 4
+tail -1 gpurun_out/r03k/smoke.txt
 s=$(date +%s.%N)
 timeout -k 10 600 python bench.py > gpurun_out/r03k/bench_default.json 2> gpurun_out/r03k/bench_default.err || exit 1
 e=$(date +%s.%N)
