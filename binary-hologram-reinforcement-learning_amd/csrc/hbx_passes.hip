@@ -407,10 +407,6 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
   const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + y0;
   const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + y0;
   const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
-  // the storing waves issue ahead of the FFT work of the CU's other waves (r03n: k_col2
-  // 2.604 -> 2.590 ms mean of 5 alternated pairs; priority 3 or also over the A loads: no more,
-  // the same around k_rowfwd32's A stores: nothing; profiles/r03/setprio_ab_r03n.txt)
-  __builtin_amdgcn_s_setprio(2);
 #pragma unroll
   for (int i = 0; i < CH / 256; ++i) {
     const float2 lo = lo_r[(32 / TL) * 16 * i];   // (rounded by col2_stage_write under SK)
@@ -421,7 +417,6 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
     // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419)
     __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, kBufNT);
   }
-  __builtin_amdgcn_s_setprio(0);
 }
 
 template <int R, int SK>
@@ -672,18 +667,12 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
   const int vmid = t == 0 ? lo + JS * (R / 2) : hiB + JS * (R / 2 - 1);
   auto load_plane = [&](pk2 (&v)[R], int p) {
     const int po = p * PLB * 8;
-#ifdef HBX_RINV_PRIO
-    __builtin_amdgcn_s_setprio(2);
-#endif
 #pragma unroll
     for (int jj = 0; jj < R; ++jj) {
       const int vo = jj < R / 2 ? lo : (jj == R / 2 ? vmid : hiB);
       const int so = po + (jj < R / 2 ? JS * jj : (jj == R / 2 ? 0 : JS * (R - 1 - jj)));
       v[jj] = to_pk(buf_ld2s(rs, vo, so));
     }
-#ifdef HBX_RINV_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
   };
   float acc[R];
 #pragma unroll
