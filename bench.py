@@ -71,6 +71,50 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) started without a launcher (no WORLD_SIZE in the environment): run
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <argv>` as a CHILD process
+    -- before this process touches torch or the GPU, and never by exec -- relay rank 0's one JSON
+    line to stdout (everything else the child prints on stdout goes to stderr) and return the
+    child's exit code.  Returns None when this process is already a rank (or N = 1): the bench
+    then runs here.  One rank per GPU, 127.0.0.1 rendezvous (train-PPO.py:296-322's 8-GPU
+    caller, BASELINE configs[3])."""
+    import subprocess
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for out in proc.stdout:
+        try:
+            obj = json.loads(out)
+        except ValueError:
+            obj = None
+        if isinstance(obj, dict) and "metric" in obj:
+            line = out.strip()
+        else:
+            sys.stderr.write(out)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        print("bench.py: the ranks exited 0 without a JSON line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
 def algorithmic_bytes(N: int, P: int):
     """HBM bytes each kernel must move per job (one colour group of one env):
     k_rowfwd: read P*N^2/8 mask bits, write P*N^2/2 complex64 (half spectrum)
@@ -454,6 +498,9 @@ def rounded(passes):
 
 def main():
     args = parse()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     # the driver reads ONE JSON line from stdout: keep a handle on the real stdout and point
     # fd 1 at stderr, so library banners (RCCL prints its version block on stdout when the
     # communicator is created) cannot land on it
@@ -473,8 +520,9 @@ def main():
     rank, world, local = hd.init(backend="gloo" if rehearse else None, force=not args.no_pg)
     if rehearse:
         local = 0
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        # never measure a different number of ranks than asked for (a --gpus 8 line from one rank)
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but this run has WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     N, B = args.size, args.envs
@@ -552,13 +600,17 @@ def main():
         dom = max(passes, key=lambda n: passes[n]["avg_ms"])
         d = passes[dom]
         pmc = load_pmc_traffic(N)
-        traffic = None
+        traffic, traffic_src = None, None
         if pmc and dom in pmc.get("kernels", {}):
             kinfo = pmc["kernels"][dom]
             if kinfo.get("jobs_per_launch") == d["jobs_per_launch"] and kinfo.get("N") == N:
                 traffic = kinfo.get("hbm_bytes_per_launch")
+                traffic_src = (f"committed rocprofv3 PMC passes (profiles/pmc_latest{'' if N == 1024 else '_' + str(N)}"
+                               f".json, source {pmc.get('source')}), a 1-GPU run of the same kernel and "
+                               f"launch shape -- not measured in this run")
         roofline = {"bound": "hbm", "achieved": round(d["achieved_GBs"], 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(d["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src,
                     "kernel": dom, "kernel_avg_ms": round(d["avg_ms"], 4),
                     "timing": f"hipEvent pairs on the launch stream around every {args.timing_every}-th launch "
                               f"of each pass inside the timed loop ({d['launches']} launches of {dom})"}
@@ -696,6 +748,9 @@ def main():
                 "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ps[dom]["achieved_GBs"], 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ps[dom]["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": mtraffic,
+                             "traffic_source": None if mtraffic is None else
+                             f"committed rocprofv3 PMC passes (profiles/pmc_latest_256.json, source "
+                             f"{pmc.get('source')}) -- not measured in this run",
                              "kernel_avg_ms": round(ps[dom]["avg_ms"], 4)},
                 "passes": rounded(ps),
                 "note": "configs[0] / train-PPO.py's env (env.py, 256x256, 1 colour group x 8 planes at 515 nm), "

@@ -489,7 +489,7 @@ int hbx_env_reset(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, const
                       planes ? e->plane_slot : nullptr);
   if (rc) return rc;
   HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, e->state_bytes, e->intensity, e->recon, e->recon_pending,
-                               CH, pd.G, (size_t)pd.N * pd.N, st));
+                               0, CH, pd.G, (size_t)pd.N * pd.N, st));
   return HBX_OK;
 }
 
@@ -498,7 +498,10 @@ int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, co
   int rc = check_plan(p);
   if (rc) return rc;
   if (!e) return fail(HBX_ERR_INVALID, "null env buffers");
-  if (what & ~(HBX_OBS_STATE | HBX_OBS_RECON)) return fail(HBX_ERR_INVALID, "what: HBX_OBS_STATE | HBX_OBS_RECON");
+  if (what & ~(HBX_OBS_STATE | HBX_OBS_RECON | HBX_OBS_RESOLVE))
+    return fail(HBX_ERR_INVALID, "what: HBX_OBS_STATE | HBX_OBS_RECON | HBX_OBS_RESOLVE");
+  if ((what & HBX_OBS_RESOLVE) && !(what & HBX_OBS_RECON))
+    return fail(HBX_ERR_INVALID, "HBX_OBS_RESOLVE is a modifier of HBX_OBS_RECON");
   const bool st_on = (what & HBX_OBS_STATE) != 0, rc_on = (what & HBX_OBS_RECON) != 0;
   if (st_on && (!e->mask || !e->state_bytes)) return fail(HBX_ERR_INVALID, "HBX_OBS_STATE needs mask and state_bytes");
   if (rc_on && (!e->recon || !e->intensity || !e->recon_pending))
@@ -509,7 +512,8 @@ int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, co
   HBX_HIP(hipSetDevice(p->device));
   const PlanDev& pd = p->pd;
   HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, st_on ? e->state_bytes : nullptr, e->intensity,
-                               rc_on ? e->recon : nullptr, e->recon_pending, pd.G * pd.P, pd.G,
+                               rc_on ? e->recon : nullptr, e->recon_pending, (what & HBX_OBS_RESOLVE) ? 1 : 0,
+                               pd.G * pd.P, pd.G,
                                (size_t)pd.N * pd.N, (hipStream_t)stream));
   return HBX_OK;
 }

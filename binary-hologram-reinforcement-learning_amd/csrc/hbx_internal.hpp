@@ -287,7 +287,7 @@ hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* i
 // plane cache (ABI v9): slot[env][i] = i for the listed envs (env_ids nullable: 0 .. n_ids - 1)
 hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CH, hipStream_t st);
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
-                           const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
+                           float* intensity, float* recon, int32_t* pending, int resolve, int CH, int G, size_t hw,
                            hipStream_t st);
 
 }  // namespace hbx

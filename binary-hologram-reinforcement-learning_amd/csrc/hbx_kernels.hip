@@ -401,10 +401,15 @@ __global__ void k_recon_reconcile(const int32_t* __restrict__ pending, float* __
 }
 
 // rebuild the observation mirrors of listed envs: state_bytes from the mask bits (one
-// 64-bit word -> 64 bytes per thread), recon <- intensity, pending <- 0.  grid (x, n_ids)
+// 64-bit word -> 64 bytes per thread), recon <- intensity (pending cleared by k_pending_clear
+// after this launch: every block of an env reads pending first).  resolve (HBX_OBS_RESOLVE):
+// an accepted step's pending reconcile (pending = g + 1: recon holds group g's new intensity,
+// the intensity cache the old one) is applied first, i.e. group g goes recon -> intensity; without
+// it intensity is authoritative (reset / checkpoint load rewrote it).  grid (x, n_ids)
 __global__ void k_obs_sync(const int32_t* __restrict__ env_ids, const uint64_t* __restrict__ mask,
-                           int8_t* __restrict__ state_bytes, const float* __restrict__ intensity,
-                           float* __restrict__ recon, int32_t* __restrict__ pending, int CH, int G, size_t hw) {
+                           int8_t* __restrict__ state_bytes, float* __restrict__ intensity,
+                           float* __restrict__ recon, const int32_t* __restrict__ pending, int resolve, int CH,
+                           int G, size_t hw) {
   const int i = blockIdx.y;
   const int e = env_ids ? env_ids[i] : i;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -426,11 +431,19 @@ __global__ void k_obs_sync(const int32_t* __restrict__ env_ids, const uint64_t* 
     }
   }
   if (recon) {
-    const float4* s = reinterpret_cast<const float4*>(intensity + (size_t)e * G * hw);
-    float4* d = reinterpret_cast<float4*>(recon + (size_t)e * G * hw);
-    for (size_t k = t0; k < (size_t)G * hw / 4; k += stride) d[k] = s[k];
-    if (t0 == 0 && pending) pending[e] = 0;
+    const int p = (resolve && pending) ? pending[e] : 0;
+    const size_t gacc = p > 0 ? (size_t)(p - 1) : (size_t)G;     // G: no group goes recon -> intensity
+    float4* in4 = reinterpret_cast<float4*>(intensity + (size_t)e * G * hw);
+    float4* rc4 = reinterpret_cast<float4*>(recon + (size_t)e * G * hw);
+    for (size_t k = t0; k < (size_t)G * hw / 4; k += stride) {
+      if (k / (hw / 4) == gacc) in4[k] = rc4[k];
+      else rc4[k] = in4[k];
+    }
   }
+}
+__global__ void k_pending_clear(const int32_t* __restrict__ env_ids, int n_ids, int32_t* __restrict__ pending) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_ids) pending[env_ids ? env_ids[i] : i] = 0;
 }
 
 // psnr from chan_stats
@@ -546,11 +559,13 @@ hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* sl
 }
 
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
-                           const float* intensity, float* recon, int32_t* pending, int CH, int G, size_t hw,
+                           float* intensity, float* recon, int32_t* pending, int resolve, int CH, int G, size_t hw,
                            hipStream_t st) {
   if (n_ids <= 0 || (!state_bytes && !recon)) return hipSuccess;
   hipLaunchKernelGGL(k_obs_sync, dim3(64, n_ids), dim3(256), 0, st, env_ids, mask, state_bytes, intensity, recon,
-                     pending, CH, G, hw);
+                     pending, resolve, CH, G, hw);
+  if (recon && pending)
+    hipLaunchKernelGGL(k_pending_clear, dim3((n_ids + 255) / 256), dim3(256), 0, st, env_ids, n_ids, pending);
   return hipGetLastError();
 }
 hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, double count, int rel,

@@ -372,28 +372,55 @@ template <int R>
 // ITER 4 = 0.152 ms, 2 = 0.144; ITER 1 timed 0.142 but wrote wrong B rows (193-223, odd, in
 // workgroups >= 256 only; not an uninitialised-LDS read: NaN-filled scratch changes nothing)
 // -- not understood, so not used (profiles/r03/kcol2_iter1_anomaly.txt).
+#ifdef HBX_COL2_ITER1   // r04 re-check of the ITER = 1 anomaly with soffset-0 stage stores (exp build only)
+__host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : 1; }
+#else
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
+#endif
 
 // N = 1024 / 256: the output line sets of a k_col2 block (TL lines: group g = slot g of
 // slot tile st, TileB) go out through the FFT scratch.  col2_stage_write: each group
 // writes its line (imaginary part times sy) into its OWN scratch region (the group's FFT
-// is done with it; no block barrier) in row order, shifted by (g / 2) * 64 / TL float2 (the
-// bank shift that makes the readers' b64 loads conflict-free).  After a block barrier,
+// is done with it; no block barrier), row y at col2_pos(g / 2, y).  After a block barrier,
 // col2_stage_store: the block stores the set as 16-B chunks (slots 2 sp, 2 sp + 1 from
 // regions 2 sp, 2 sp + 1) in memory order -- one contiguous run per 16-row band.
 template <int R>
 constexpr int col2_region_stride() { return R * (R + 1) > R * R + 32 ? R * (R + 1) : R * R + 32; }
 template <int R>
 __device__ __forceinline__ float2* col2_region(float2* scratch, int g) {
-  return scratch + g * col2_region_stride<R>() + (g >> 1) * (64 / (256 / R));
+  return scratch + g * col2_region_stride<R>();
+}
+// Where row y of slot pair sp's regions sits.  The readers (col2_stage_store) load the rows
+// y0 = band * 16 + (tid / NSP) % 16 of the NSP = TL / 2 slot pairs sp = tid % NSP; gfx950 serves
+// the compiler's ds_read2(st64)_b64 as 16-lane groups over 32 banks (16 float2: NSP pairs x
+// 16 / NSP rows) and a ds_read_b64 as 32-lane groups over 64 banks (NSP pairs x 32 / NSP rows).
+// A constant shift per pair cannot serve both (r03's (sp * 64 / TL) was the 64-bank one; the
+// compiler emits read2st64, and rocprofv3 counted 67.1 M SQ_LDS_BANK_CONFLICT cycles per 128-job
+// k_col2 launch = 8 extra cycles on each of the 32 stage reads per wave and line).  Shift sp by
+// 32 / TL float2 and flip row bit 4 (+16 banks) when row bit HB (the bit splitting a 32-lane
+// group's rows in halves) is set, except for the last pair: conflict-free in both models, and
+// the writers' 16-lane runs of consecutive rows stay conflict-free (tools/lds_swizzle_model.py
+// checks all three; found by exhaustive search over this family).
+template <int R>
+__device__ __forceinline__ int col2_pos(int sp, int y) {
+  constexpr int TL = 256 / R, NSP = TL / 2, HB = ilog2c(16 / NSP);
+  return sp * (32 / TL) + (y ^ ((((y >> HB) & 1) && sp != NSP - 1) ? 16 : 0));
 }
 
 template <int R, int SK>
 __device__ __forceinline__ void col2_stage_write(const float2 (&v)[R], float sy, float2* scratch, int grp, int t) {
+  // row y = t + R k2: col2_pos only touches bits < 5, so rows R q apart with R q a multiple of
+  // 32 share a lane base (constant offsets, the stores pair into ds_write2_b64)
+  constexpr int PQ = R >= 32 ? 1 : 32 / R;
   float2* reg = col2_region<R>(scratch, grp);
+  float2* base[PQ];
 #pragma unroll
-  for (int k2 = 0; k2 < R; ++k2)   // row y = t + R k2
-    reg[R * k2 + t] = store_round<SK>(make_float2(v[k2].x, sy * v[k2].y));
+  for (int q = 0; q < PQ; ++q) base[q] = reg + col2_pos<R>(grp >> 1, t + R * q);
+#pragma unroll
+  for (int q = 0; q < PQ; ++q) {
+#pragma unroll
+    for (int k2 = q; k2 < R; k2 += PQ) base[q][R * (k2 - q)] = store_round<SK>(make_float2(v[k2].x, sy * v[k2].y));
+  }
 }
 
 template <int R>
@@ -404,8 +431,10 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
   const int tid = threadIdx.x, sp = tid % (TL / 2);
   const int band0 = tid / (8 * TL), r = (tid / (TL / 2)) % 16;
   const int y0 = band0 * 16 + r;
-  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + y0;
-  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + y0;
+  // rows y0 + (32 / TL) 16 i differ from y0 in bits >= 5 only, so col2_pos moves with them
+  static_assert((32 / TL) * 16 >= 32, "stage rows step past the swizzled bits");
+  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + col2_pos<R>(sp, y0);
+  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + col2_pos<R>(sp, y0);
   const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
 #pragma unroll
   for (int i = 0; i < CH / 256; ++i) {
@@ -414,8 +443,14 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
     const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
     // non-temporal (nt): B streams out without taking Infinity-Cache residency, so its write-back
     // no longer lands on top of k_rowinv's reads (r03: N = 256 k_col2 0.143 -> 0.128 ms and
-    // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419)
-    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff, (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, kBufNT);
+    // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419).
+    // soffset stays the literal 0, the whole offset rides in voffset: LLVM's gfx950 hazard
+    // recognizer inserts the 2 wait states a VALU write of a >64-bit store's data VGPRs needs
+    // only when the MUBUF soffset is not a register -- with an SGPR soffset (r03) it assumed no
+    // hazard and scheduled such writes right behind the store, the cause of the r03 bf16
+    // non-determinism and of the ITER = 1 wrong B rows (tools/hazard_scan.py
+    // now rejects any wide buffer store with a register soffset)
+    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff + (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, 0, kBufNT);
   }
 }
 

@@ -958,6 +958,12 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   if constexpr (!PERSIST) {
     return;
   } else {
+    // a waiting block that timed out stored fault = done = 1 with sc1 stores; the state this
+    // block built came from the batch start (fault 0), so re-read the abort word and keep them
+    if (tid == 0 && __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      s_ws.fault = 1;
+      s_ws.done = 1;
+    }
     __syncthreads();
     if (tid < kWsWords)
       __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&s_ws)[tid], r_ws, tid * 4, 0, kSc1);

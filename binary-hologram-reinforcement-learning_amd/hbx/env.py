@@ -50,11 +50,16 @@ class LazyObs(dict):
     """Dict observation kept on the GPU whose values become numpy arrays on first
     access (cached): an SB3 rollout buffer that reads every key pays one device ->
     host copy per key, a consumer that reads none pays nothing.  ``.device(key)``
-    returns the device tensor without a copy."""
+    returns the device tensor without a copy.
+
+    The env's observations are VIEWS of buffers the next step rewrites (ABI v8), so LazyObs
+    takes a device snapshot (clone) of every key when it is built: a key first read after
+    the next env.step() still shows this step's data (SB3 assigns self._last_obs into its
+    rollout buffer after the following step)."""
 
     def __init__(self, tensors: dict):
         super().__init__()
-        self._t = dict(tensors)
+        self._t = {k: v.clone() for k, v in tensors.items()}
         for k in self._t:
             dict.__setitem__(self, k, None)
 
@@ -398,10 +403,22 @@ class HologramVecEnv(_VecEnvBase):
             self.plan.env_step(self.state.bufs, self.params, self.num_envs, actions, *out)
         return out
 
+    def _graph_key(self):
+        """What a captured step bakes in by value: the EnvParams fields (kernel arguments) and
+        the plan's per-call state (timing, precision)."""
+        p = self.params
+        return (self.plan.generation, p.max_steps, p.t_psnr, p.t_steps, p.t_psnr_diff, p.reward_weight,
+                p.accept_rule, p.reward_kind)
+
     def _graph_step(self, actions: torch.Tensor):
         """hbx_env_step replayed from a captured HIP graph (static buffers: the env's own
         state and output row, a static action vector).  Capture records the launches without
-        running them; the replay right after runs this step."""
+        running them; the replay right after runs this step.  A HIP graph keeps the kernel
+        arguments it was captured with, so a change of the EnvParams (set_attr('max_steps', ..),
+        a direct write to env.params) or of the plan's timing / precision drops the graph and
+        the next step captures afresh."""
+        if self._graph is not None and self._graph_key_captured != self._graph_key():
+            self._graph = None
         if self._graph is None:
             self._g_actions = actions.clone()
             out = (self._reward, self._psnr, self._acc, self._term, self._trunc)
@@ -417,6 +434,7 @@ class HologramVecEnv(_VecEnvBase):
                 self.plan.env_step(self.state.bufs, self.params, self.num_envs, self._g_actions, *out)
             torch.cuda.current_stream(self.device).wait_stream(s)
             self._graph = g
+            self._graph_key_captured = self._graph_key()
         self._g_actions.copy_(actions)
         self._graph.replay()
 

@@ -150,6 +150,9 @@ class Plan:
             _lib.check(self.lib.hbx_plan_create(C.byref(h), C.byref(oc), self.max_jobs,
                                                 self.device_index), "hbx_plan_create")
         self._h = h
+        # bumped by every call that changes what a launch sequence records (timing events,
+        # precision variant): a captured HIP graph of this plan's launches is stale after it
+        self.generation = 0
         if precision != _lib.PRECISION_F32:
             self.precision = precision
 
@@ -173,6 +176,7 @@ class Plan:
         """Record up to `capacity` launches per pass, every `every`-th launch."""
         _lib.check(self.lib.hbx_plan_set_timing_sampled(self._h, int(capacity), int(every)),
                    "hbx_plan_set_timing_sampled")
+        self.generation += 1
 
     def read_timing(self):
         """{pass: (total_ms, launches, jobs)} for k_rowfwd / k_col / k_rowinv (syncs)."""
@@ -196,6 +200,7 @@ class Plan:
         """PRECISION_F32 (the product path) or the bf16 / fp16 intermediate-storage
         numerics of SURVEY 8d cfg 5 (DBS_ratio_0.5.py fp32 vs bf16 sweep)."""
         _lib.check(self.lib.hbx_plan_set_precision(self._h, int(kind)), "hbx_plan_set_precision")
+        self.generation += 1
 
     @property
     def pipeline(self) -> int:

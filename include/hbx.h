@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 9
+#define HBX_ABI_VERSION 10
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -363,11 +363,18 @@ int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_en
 /* (ABI v8) Rebuild the observation mirrors of the listed envs (env_ids
  * nullable = all n_env) from the state they mirror:
  *   HBX_OBS_STATE  state_bytes <- the mask bits
- *   HBX_OBS_RECON  recon <- intensity, recon_pending <- 0
+ *   HBX_OBS_RECON  recon <- intensity, recon_pending <- 0; the intensity cache is
+ *                  taken as authoritative (it was just rewritten: reset, checkpoint load)
+ *   HBX_OBS_RESOLVE (ABI v10, with HBX_OBS_RECON) apply the last step's pending
+ *                  reconcile first: after an accepted step the stepped group's new
+ *                  intensity lives in recon only (recon_pending = group + 1), so that
+ *                  group goes recon -> intensity and the others intensity -> recon.
+ *                  Use it to re-sync mid-episode without rewriting intensity.
  * hbx_env_reset does both for the envs it resets; a caller that restores
  * masks or intensities by itself (checkpoint load) calls it after. */
 #define HBX_OBS_STATE 1
 #define HBX_OBS_RECON 2
+#define HBX_OBS_RESOLVE 4
 int hbx_env_obs_sync(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
                      const int32_t* env_ids, int32_t n_ids, int32_t what, void* stream);
 

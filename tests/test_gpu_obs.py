@@ -167,3 +167,85 @@ def test_graph_replayed_step_equals_eager(mode):
     assert graph._graph is not None and n_done > 0
     for key in ("mask", "chan_stats", "prev_psnr", "steps", "flip_count"):
         assert torch.equal(getattr(eager.state, key), getattr(graph.state, key)), key
+
+
+def test_graph_step_follows_set_attr_and_plan_changes():
+    """a HIP graph keeps the kernel arguments it was captured with, and
+    EnvParams go to k_env_step_finalize by value.  After set_attr('max_steps' / 'T_PSNR', ...)
+    or a plan timing change the graph-replayed env must behave as the eager env does."""
+    import hbx
+    from hbx.env import HologramVecEnv
+    cfg = hbx.mono_config(256)
+    B = 6
+    g = torch.Generator(device="cuda").manual_seed(31)
+    pres = [torch.rand((cfg.channels, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=1000, T_PSNR=1e9,
+              T_PSNR_DIFF=1e9)
+    eager = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    graph = HologramVecEnv(cfg, B, lambda i: tgts[i], graph=True, **kw)
+    eager.reset()
+    graph.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (60, B), generator=g, device="cuda")
+    truncs = 0
+    for k in range(60):
+        if k == 5:                                      # after the graph has been captured
+            assert graph._graph is not None
+            for e in (eager, graph):
+                e.set_attr("max_steps", 12)
+        if k == 30:
+            for e in (eager, graph):
+                e.set_attr("max_steps", 1000)
+                e.set_attr("T_PSNR", 0.0)               # every accepted step now counts as sustained
+                e.set_attr("T_PSNR_DIFF", -1e9)
+        if k == 40:
+            graph.plan.set_timing(64, 2)                # plan per-call state changes: recapture
+        o1, r1, d1, i1 = eager.step(acts[k])
+        o2, r2, d2, i2 = graph.step(acts[k])
+        assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
+        assert [x.get("TimeLimit.truncated") for x in i1] == [x.get("TimeLimit.truncated") for x in i2], k
+        truncs += sum(bool(x.get("TimeLimit.truncated")) for x in i1)
+    assert truncs > 0                                   # max_steps = 12 truncated episodes
+    for key in ("mask", "chan_stats", "prev_psnr", "steps", "flip_count", "sustained"):
+        assert torch.equal(getattr(eager.state, key), getattr(graph.state, key)), key
+    eager.close()
+    graph.close()
+
+
+def test_obs_sync_resolve_right_after_accepted_step():
+    """hbx_env_obs_sync(HBX_OBS_RECON) right after an accepted step used to copy
+    the stale intensity cache over the correct recon and drop the pending reconcile.  With
+    HBX_OBS_RESOLVE (ABI v10) the pending group goes recon -> intensity first; afterwards recon and
+    the intensity cache both equal the propagation of the accepted mask, pending is 0, and the env
+    keeps stepping exactly like an untouched twin."""
+    import hbx
+    from hbx import _lib
+    cfg = hbx.mono_config(256)
+    B = 4
+    env, g = _env(cfg, B, 77)
+    twin, _ = _env(cfg, B, 77)
+    env.reset()
+    twin.reset()
+    st = env.state
+    plan = hbx.Plan(cfg, max_jobs=B)
+    acts = torch.randint(0, cfg.channels * 256 * 256, (40, B), generator=g, device="cuda")
+    synced = 0
+    for k in range(40):
+        env.step(acts[k])
+        twin.step(acts[k])
+        acc = env._acc.bool()
+        if acc.any() and k % 3 == 0:
+            assert int(st.recon_pending[acc].min()) > 0
+            plan.env_obs_sync(st.bufs, B, _lib.OBS_RECON | _lib.OBS_RESOLVE)
+            i_now, _, _ = plan.propagate(st.mask, st.target)
+            assert torch.equal(st.recon, i_now) and torch.equal(st.intensity, i_now), k
+            assert int(st.recon_pending.abs().sum()) == 0
+            synced += 1
+        assert torch.equal(env.state.recon, twin.state.recon), k
+        assert torch.equal(env.state.prev_psnr, twin.state.prev_psnr), k
+    assert synced > 0
+    with pytest.raises(_lib.HbxError):
+        plan.env_obs_sync(st.bufs, B, _lib.OBS_RESOLVE)         # a modifier of OBS_RECON only
+    plan.close()
+    env.close()
+    twin.close()
