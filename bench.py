@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-scipy", action="store_true", help="skip the multi-core scipy CPU baseline")
     ap.add_argument("--no-probe", action="store_true", help="skip the all-flip probe-sweep measurement")
     ap.add_argument("--no-ppo", action="store_true", help="skip the 256x256x8 mono (train-PPO) measurement")
+    ap.add_argument("--no-crop", action="store_true",
+                    help="skip the 896 x 896 centre-crop line (env_1024_24_128.py:144-149)")
     ap.add_argument("--no-obs", action="store_true",
                     help="skip the SB3-facing step with all five observations (vecenv_step_obs)")
     ap.add_argument("--no-precision", action="store_true",
@@ -510,7 +512,7 @@ def main():
     import torch
     from hbx import dist as hd
     from hbx.env import HologramVecEnv
-    from hbx.plan import mono_config, rgb_config
+    from hbx.plan import crop_config, mono_config, rgb_config
 
     # HBX_BENCH_REHEARSE_ONE_GPU=1: every rank on cuda:0 over gloo -- rehearses the world > 1
     # code path on a one-GPU box (RCCL refuses two ranks on one device); never a measurement
@@ -539,15 +541,16 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1_000_003 * (rank * B + i))
         return torch.rand((CH, N, N), generator=g, device="cuda")
 
-    def measure(mode: str, steps: int, warmup: int, mcfg=None, timing_every=None):
+    def measure(mode: str, steps: int, warmup: int, mcfg=None, timing_every=None, margin=0):
         mcfg = mcfg or cfg
         mG, mCH, mN = mcfg.groups, mcfg.channels, mcfg.height
+        m0 = margin       # centre crop (env_1024_24_128.py:144-149) or the top-left corner
 
         def tsrc(i):
-            return target_source(i)[:mG, :mN, :mN].contiguous()
+            return target_source(i)[:mG, m0:m0 + mN, m0:m0 + mN].contiguous()
 
         def psrc(i):
-            return pre_model_source(i)[:mCH, :mN, :mN].contiguous()
+            return pre_model_source(i)[:mCH, m0:m0 + mN, m0:m0 + mN].contiguous()
 
         vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=(),
                              auto_reset=False, max_steps=10 ** 9, max_jobs=args.chunk or None, mode=mode,
@@ -722,6 +725,41 @@ def main():
                         "the flipped plane's pair and sums the other planes' cached |U|^2 in the FFT mode's "
                         "plane order (include/hbx.h ABI v9); reported separately, the headline stays the "
                         "literal re-propagation of the whole group"}
+        torch.cuda.empty_cache()
+
+    if not args.no_crop and N == 1024:
+        # env_1024_24_128.py:144-149 (BASELINE configs[2]'s script): the centre 896 x 896 crop of
+        # the 1024 masks, 24 planes, 128 envs per GPU, FFT mode -- the mixed-radix 28 x 32 passes
+        ccfg = crop_config(cfg, 64)
+        cN = ccfg.height
+        vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup, mcfg=ccfg, margin=64)
+        vec.close()
+        if rank == 0:
+            cb = algorithmic_bytes(cN, P)
+            ps = pass_table(timing, cb)
+            dom = max(ps, key=lambda n: ps[n]["avg_ms"])
+            pmc = load_pmc_traffic(cN)
+            ctraffic, csrc = None, None
+            if pmc and dom in pmc.get("kernels", {}):
+                kinfo = pmc["kernels"][dom]
+                if kinfo.get("jobs_per_launch") == ps[dom]["jobs_per_launch"] and kinfo.get("N") == cN:
+                    ctraffic = kinfo.get("hbm_bytes_per_launch")
+                    csrc = (f"committed rocprofv3 PMC passes (profiles/pmc_latest_{cN}.json, source "
+                            f"{pmc.get('source')}) -- not measured in this run")
+            cms = dt / args.steps * 1e3
+            cstep = sum(cb[k] for k in ("k_rowfwd", "k_col", "k_rowinv")) * B
+            out["crop_896"] = {
+                "value": round(B * world * args.steps / dt, 2), "unit": "env-steps/s", "envs_per_gpu": B,
+                "steps": args.steps, "ms_per_step": round(cms, 4), "accept_rate": round(acc_rate, 4),
+                "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ps[dom]["achieved_GBs"], 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ps[dom]["achieved_GBs"] / HBM_PEAK_GBS, 4), "traffic": ctraffic,
+                             "traffic_source": csrc, "kernel_avg_ms": round(ps[dom]["avg_ms"], 4)},
+                "passes": rounded(ps),
+                "step_alg_frac": round(cstep / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "note": "env_1024_24_128.py:144-149: the centre 896 x 896 crop of 1024 x 1024 x 24 masks "
+                        "(64 px per side), FFT mode, same env semantics; 896 = 28 x 32 mixed-radix passes "
+                        "(csrc/hbx_passes896.hip)"}
         torch.cuda.empty_cache()
 
     if world == 1 and not args.no_ppo:

@@ -610,6 +610,35 @@ __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch&
   else dft_reg<32, INV>(v);
 }
 
+// fft896_ns with half the scratch (r04, k_rowfwd896 at three workgroups per CU): the transpose
+// moves the real parts, then the imaginary parts, through a private [32][33] FLOAT tile
+// (fft_group_split's scheme).  Same arithmetic, bit-identical result.
+template <bool INV>
+__device__ __forceinline__ void fft896_ns_split(float2 (&v)[32], int t, float* sc, const float2* tw896) {
+  asm volatile("" ::: "memory");
+  dft28_pk<INV>(v);
+#pragma unroll
+  for (int k1 = 1; k1 < 28; ++k1) {
+    const pk2 w = to_pk(tw896[k1 * 32 + t]);
+    v[k1] = from_pk(INV ? pk_cmulc(to_pk(v[k1]), w) : pk_cmul(to_pk(v[k1]), w));
+  }
+  const int k1 = t < 28 ? t : 0;
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < 28; ++j) sc[t * 33 + j] = v[j].x;
+  wave_sync();
+#pragma unroll
+  for (int tt = 0; tt < 32; ++tt) v[tt].x = sc[tt * 33 + k1];
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < 28; ++j) sc[t * 33 + j] = v[j].y;
+  wave_sync();
+#pragma unroll
+  for (int tt = 0; tt < 32; ++tt) v[tt].y = sc[tt * 33 + k1];
+  wave_sync();
+  dft_reg<32, INV>(v);
+}
+
 // 896-point FFT by 32 lanes, slot layout in -> natural layout out (adjoint of
 // fft896_ns: the same stages in reverse order with the opposite sign)
 template <bool INV, bool SCALAR = false, class Scratch>

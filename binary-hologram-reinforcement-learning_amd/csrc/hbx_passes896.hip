@@ -59,111 +59,156 @@ __device__ __forceinline__ float2 mirror_conj896(const float2 (&v)[32], int k2, 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// Pass 1
+// Pass 1 (r04: k_rowfwd32's scheme at 896)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_rowfwd896(const JobDesc* __restrict__ jobs,
+// A at 896 is stored in panels of the row block height, [y / 8][kx < 448][y % 8] (r01-r03:
+// line-major [kx][y], i.e. 64-B pieces of every line per row block -- the access shape that
+// replayed at 1.19-1.24 ms against 0.69 ms for contiguous panels at N = 1024, DESIGN.md 4;
+// k_rowfwd896 ran at 0.40 of 8 TB/s).  A row block now writes one contiguous 28-KB panel per
+// plane, and k_col896's lane groups read 64-B pieces of 8 consecutive y.
+__host__ __device__ constexpr size_t a896_at(int kx, int y) {
+  return (size_t)(y >> 3) * (kHalf * kGPB) + (size_t)kx * kGPB + (y & 7);
+}
+
+// Three workgroups per CU, as k_rowfwd32 (hbx_passes.hip): lane t < 28 loads mask word t of
+// its row (lanes 28..31 re-load word 27; their bits land in bits 28..31 of the transposed
+// words, x >= 896, never used) and group_bit_transpose hands lane t bit t of every word;
+// the FFT transposes real then imaginary parts through a 4.2-KB float tile per group
+// (fft896_ns_split); the Hermitian split goes out one plane at a time through a 28-KB tile
+// aliasing those FFT tiles; each workgroup walks RIT896 row blocks of one plane pair with the
+// next rows' words loaded before the stores; A is stored non-temporal.
+// Tile of one plane's half spectrum [kx < 448][8 rows] for k_rowfwd896, row r XOR-swizzled by
+// a function of kx mod 28: the lane-row writes (lane t: kx = t + 28 k2) then address one
+// lane base + k2 * 28 * 8 (tile_pos<32, 8>'s swizzle keys on kx mod 32, which pinned 16 address
+// VGPRs and spilled at three workgroups per CU), and are conflict-free; the 16-B chunk reads
+// are conflict-free as 16-lane read2 and 16 extra cycles per 56 reads as ds_read_b64
+// (exhaustive search over ((m >> a) & 7) ^ b * bit c of m, tools/lds_swizzle_model.py)
+__device__ __forceinline__ int tile896_pos(int kx, int r) {
+  const int m = kx % kL;
+  return kx * kGPB + (r ^ ((((m >> 2) & 7) ^ (((m >> 1) & 1) * 5)) & 7));
+}
+
+constexpr int kRit896 = 4;                       // row blocks per workgroup (112 / 4 = 28 per pair)
+static_assert(kRB % kRit896 == 0, "row-block walk");
+
+__global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict__ jobs,
                                                       const uint32_t* __restrict__ mask,
                                                       float2* __restrict__ ws_a,
                                                       const float2* __restrict__ tw_glob, int P, int CH,
                                                       float va, float vb) {
+  constexpr int SCRF = kGPB * kR * (kR + 1);      // floats: 8 FFT tiles (33.8 KB)
+  static_assert(kHalf * kGPB * 2 <= SCRF, "one plane's tile must fit in the FFT tiles");
+  constexpr int RBW = kRB / kRit896;
   __shared__ float2 tw[kN];
-  __shared__ __attribute__((aligned(16))) float2 lds[kSCR];
+  __shared__ __attribute__((aligned(16))) float lds[SCRF];
   for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
 
   const int grp = threadIdx.x / kR;
   const int t = threadIdx.x % kR;
   const int lane_base = (threadIdx.x & 63) - t;
-  int bid = xcd_pair<kRB>(blockIdx.x);
-  const int rb = bid % kRB;
-  bid /= kRB;
+  int bid = blockIdx.x;
+  const int rbw = bid % RBW;
+  bid /= RBW;
   const int q = bid % (P / 2);
   const int j = bid / (P / 2);
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;  // uniform per block
-  const int y0 = rb * kGPB;
-  const int y = y0 + grp;
   const int pa = 2 * q, pb = 2 * q + 1;
+  const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * kN * kWPR;
+  const int wt = t < kWPR ? t : kWPR - 1;
+  uint32_t wa, wb;
+  auto load_row = [&](int y) {
+    wa = plane_a[(size_t)y * kWPR + wt];
+    wb = plane_a[(size_t)(kN + y) * kWPR + wt];
+  };
+  load_row(rbw * kRit896 * kGPB + grp);
+  __syncthreads();  // tw visible
 
-  const uint32_t* rowa = mask + ((size_t)jb.env * CH + jb.group * P + pa) * kN * kWPR + (size_t)y * kWPR;
-  const uint32_t* rowb = rowa + (size_t)kN * kWPR;
-  uint32_t wa[kWPR], wb[kWPR];
-#pragma unroll
-  for (int i = 0; i < kWPR / 4; ++i) {
-    const uint4 a = reinterpret_cast<const uint4*>(rowa)[i];
-    const uint4 b = reinterpret_cast<const uint4*>(rowb)[i];
-    wa[4 * i] = a.x; wa[4 * i + 1] = a.y; wa[4 * i + 2] = a.z; wa[4 * i + 3] = a.w;
-    wb[4 * i] = b.x; wb[4 * i + 1] = b.y; wb[4 * i + 2] = b.z; wb[4 * i + 3] = b.w;
-  }
-  if (jb.flip_plane >= 0 && jb.flip_pix / kN == y) {  // env.py:164 flip, on the fly
-    const int col = jb.flip_pix % kN;
-    const uint32_t bit = 1u << (col & 31);
-#pragma unroll
-    for (int i = 0; i < kWPR; ++i) {
-      if (i == (col >> 5)) {
-        if (jb.flip_plane == pa) wa[i] ^= bit;
-        if (jb.flip_plane == pb) wb[i] ^= bit;
+  float2* base = ws_a + ((size_t)j * P + pa) * kPlaneA;
+  float2* tile = reinterpret_cast<float2*>(lds);
+  constexpr int CHUNKS = kHalf * kGPB / 2;      // 16-B chunks of one plane's panel (1792)
+  static_assert(CHUNKS % 256 == 0, "chunking");
+#pragma unroll 1
+  for (int it = 0; it < kRit896; ++it) {
+    const int y0 = (rbw * kRit896 + it) * kGPB;
+    const int y = y0 + grp;
+    uint32_t ta = group_bit_transpose(wa, t);   // bit r = pixel x = t + 32 r of the row
+    uint32_t tb = group_bit_transpose(wb, t);
+    if (jb.flip_plane >= 0 && jb.flip_pix / kN == y) {  // env.py:164 flip, on the fly
+      const int col = jb.flip_pix % kN;
+      if (t == (col & 31)) {
+        if (jb.flip_plane == pa) ta ^= 1u << (col >> 5);
+        if (jb.flip_plane == pb) tb ^= 1u << (col >> 5);
       }
     }
-  }
-  float2 v[32];
+    float2 v[32];
 #pragma unroll
-  for (int jj = 0; jj < kL; ++jj)   // x = t + 32 jj is bit t of word jj
-    v[jj] = make_float2(fmaf(vb, (float)((wa[jj] >> t) & 1u), va), fmaf(vb, (float)((wb[jj] >> t) & 1u), va));
+    for (int jj = 0; jj < kL; ++jj)
+      v[jj] = make_float2(fmaf(vb, (float)((ta >> jj) & 1u), va), fmaf(vb, (float)((tb >> jj) & 1u), va));
 #pragma unroll
-  for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
-  __syncthreads();  // tw visible
-  fft896_ns<false>(v, t, PaddedScratch<kR>{lds + grp * kR * (kR + 1)}, tw);
-  lds_barrier();    // every group is done with its scratch: reuse as the tile
+    for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
+    // next rows' words (the last iteration re-reads its own row: no conditional load)
+    load_row(it + 1 < kRit896 ? y + kGPB : y);
+    if (it > 0) lds_barrier();   // every group has read the previous plane-b tile
+    fft896_ns_split<false>(v, t, lds + grp * kR * (kR + 1), tw);
 
-  // Hermitian split of the slot-layout spectrum (kx = t + 28 k2 < 448: k2 < 16)
-  float2* tile = lds;
-  const float2 zny = v[16];  // Z[448] on lane 0
+    // Hermitian split of the slot-layout spectrum (kx = t + 28 k2 < 448: k2 < 16): plane a
+    // now, plane b kept in registers for the second tile
+    float2 fb[16];
+    lds_barrier();    // every group is done with its FFT tile: reuse as the plane tile
+    const float2 zny = v[16];  // Z[448] on lane 0
 #pragma unroll
-  for (int k2 = 0; k2 < 16; ++k2) {
-    const float2 z = v[k2];
-    const float2 m = mirror_conj896(v, k2, t, lane_base);
-    float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-    float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
-    if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
-      fa = make_float2(z.x, zny.x);
-      fb = make_float2(z.y, zny.y);
+    for (int k2 = 0; k2 < 16; ++k2) {
+      const float2 z = v[k2];
+      const float2 m = mirror_conj896(v, k2, t, lane_base);
+      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
+      fb[k2] = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
+        fa = make_float2(z.x, zny.x);
+        fb[k2] = make_float2(z.y, zny.y);
+      }
+      if (t < kL) tile[tile896_pos(t + kL * k2, grp)] = fa;
     }
-    if (t < kL) {
-      const int kx = t + kL * k2;
-      tile[tile_pos<kR, kGPB>(kx, grp)] = fa;
-      tile[tile_pos<kR, kGPB>(kHalf + kx, grp)] = fb;
-    }
-  }
-  lds_barrier();
-  // A[pa|pb][kx][y0 .. y0+8): 16 B per thread per chunk
-  float2* base = ws_a + ((size_t)j * P + pa) * kPlaneA;
-  constexpr int CHUNKS = kN * kGPB / 2;
-  static_assert(CHUNKS % 256 == 0, "chunking");
 #pragma unroll
-  for (int i = 0; i < CHUNKS / 256; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    const int r2 = (c % (kGPB / 2)) * 2;
-    const int line = c / (kGPB / 2);   // pl * 448 + kx
-    const float2 a = tile[tile_pos<kR, kGPB>(line, r2)];
-    const float2 b = tile[tile_pos<kR, kGPB>(line, r2 + 1)];
-    const int pl = line / kHalf;
-    st_stream4(base + (size_t)pl * kPlaneA + (size_t)(line - pl * kHalf) * kN + y0 + r2,
-               make_float4(a.x, a.y, b.x, b.y));
+    for (int pl = 0; pl < 2; ++pl) {
+      if (pl == 1) {
+        lds_barrier();   // plane a's tile has been read
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2)
+          if (t < kL) tile[tile896_pos(t + kL * k2, grp)] = fb[k2];
+      }
+      lds_barrier();
+      float2* panel = base + (size_t)pl * kPlaneA + a896_at(0, y0);
+#pragma unroll
+      for (int i = 0; i < CHUNKS / 256; ++i) {
+        const int c = threadIdx.x + 256 * i;
+        const int r2 = (c % (kGPB / 2)) * 2;
+        const int line = c / (kGPB / 2);
+        const float2 a = tile[tile896_pos(line, r2)];
+        const float2 b = tile[tile896_pos(line, r2 + 1)];
+        st_stream4(panel + 2 * c, make_float4(a.x, a.y, b.x, b.y));   // = a896_at(line, y0 + r2)
+      }
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pass 2: one lane group per input line and both of its output lines (as
-// k_col2): FFT over y -> Z (slot layout); W = Z conj H to the group's scratch
-// (+ a pad copy of W[0]) while v becomes Z H; M H = conj W(N - ky) read back
-// (H is even in ky); IFFT of Z H -> B line kx, of M H -> B line N - kx
-// (kx = 0: (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448)
+// Pass 2 (r04: k_col2's scheme at 896): one lane group per input line and both of its
+// output lines.  FFT over y -> Z (slot layout); H(kx, ky) for ky <= 448 only (17 of 32
+// registers; H is even in ky, the other 15 come mirrored through the group's scratch);
+// v <- Z H -> IFFT -> B line kx; w <- Z conj H -> IFFT -> conj -> B line N - kx (the
+// conjugate-even identity of k_col2, no mirror of the line).  kx = 0: (Z + M)/2 H(0) ->
+// line 0, -i (Z - M)/2 H(448) -> line 448 with M = conj Z(-ky) from a register shuffle.
+// XCD-aware lines: the 8 line blocks of a plane are blockIdx % 8, i.e. one per XCD (blocks
+// are dispatched round-robin over the 8 XCDs; placement is a speed hint only), so an XCD
+// touches only its 56 of the 448 H rows of each colour group -- 0.2 MB per group in its
+// 4-MB L2 instead of the whole 3.2-MB table (r03: 1.22x the algorithmic bytes, the H rows
+// re-fetched across jobs of different colour groups).
 // ---------------------------------------------------------------------------
-constexpr bool kColScalar = true;    // packed 32-point DFTs spill with two lines live
 constexpr bool kInvScalar = false;   // k_rowinv896: packed DFTs (one line live)
-constexpr int kColIter = 4;
-constexpr int kColLB = kHalf / (kGPB * kColIter);   // 14 blocks per plane
-static_assert(kHalf % (kGPB * kColIter) == 0, "line blocking");
+constexpr int kColIter = 7;
+constexpr int kColLB = kHalf / (kGPB * kColIter);   // 8 line blocks per plane = one per XCD
+static_assert(kHalf % (kGPB * kColIter) == 0 && kColLB == 8, "line blocking");
 
 __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ jobs,
                                                    const float2* __restrict__ ws_a,
@@ -176,6 +221,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
 
   const int grp = threadIdx.x / kR;
   const int t = threadIdx.x % kR;
+  const int lane_base = (threadIdx.x & 63) - t;
   int bid = blockIdx.x;
   const int lb = bid % kColLB;
   bid /= kColLB;
@@ -187,20 +233,23 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * kPlaneB, (unsigned)(kPlaneB * 8));
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (kHalf + 1) * kN,
                                                (unsigned)((kHalf + 1) * kN * 8));
-  const PaddedScratch<kR> sc{scratch + grp * kR * (kR + 1)};
+  float2* const hs = scratch + grp * kR * (kR + 1);
+  const PaddedScratch<kR> sc{hs};
   const int k1 = t < kL ? t : 0;   // slot lane (28..31 carry don't-care values)
-  const float2* mrow = (t > 0 && t < kL) ? sc.at(kL - t, 31) : sc.at(0, 32);
+  // the mirror of ky = k1 + 28 k2 (k2 > 16) is 896 - ky = (28 - k1) + 28 (31 - k2), lane 0:
+  // 28 (32 - k2); the group wrote its ky <= 448 values as hs[k2 * 32 + lane]
+  const float2* hm = hs + ((t > 0 && t < kL) ? kL - t : kR);
+  // A line kx of a panel plane as seen by lane t: y = t + 32 jj -> a896_at(kx, t) + jj * 4 panels
+  const int lane_a = (int)a896_at(0, t) * 8;
+  constexpr int JSTEP = 4 * kHalf * kGPB * 8;   // bytes between registers jj and jj + 1
   constexpr int KSTEP = kColLB * kGPB;
   const int kx0 = lb * kGPB + grp;
 
   float2 v[32];
-  {
-    const int vo = (kx0 * kN + t) * 8;
 #pragma unroll
-    for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, vo, jj * kR * 8);
+  for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, lane_a + kx0 * kGPB * 8, jj * JSTEP);
 #pragma unroll
-    for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
-  }
+  for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
   lds_barrier();  // tw visible (the line loads stay in flight)
 
 #pragma unroll 1
@@ -208,59 +257,55 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     const int kx = kx0 + it * KSTEP;
     const bool dc = (kx == 0);
     const int vh = (kx * kN + k1) * 8;   // H(kx, ky = k1 + 28 k2) at vh + k2 * 28 * 8
-    fft896_ns<false, kColScalar>(v, t, sc, tw);
-    wave_sync();
+    float2 hb[32];
     if (!dc) {
 #pragma unroll
-      for (int c8 = 0; c8 < 32; c8 += 8) {
-        float2 hb[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) hb[i] = buf_ld2(rh, vh, (c8 + i) * kL * 8);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int k2 = c8 + i;
-          const float2 w = cmulc(v[k2], hb[i]);
-          *sc.at(t, k2) = w;
-          if (k2 == 0) *sc.at(t, 32) = w;
-          v[k2] = cmul(v[k2], hb[i]);
-        }
-      }
-    } else {  // kx = 0: plain Z through the scratch
-#pragma unroll
-      for (int k2 = 0; k2 < 32; ++k2) *sc.at(t, k2) = v[k2];
-      *sc.at(t, 32) = v[0];
+      for (int i = 0; i <= 16; ++i) hb[i] = buf_ld2(rh, vh, i * kL * 8);
     }
-    wave_sync();
-    float2 m[32];
+    fft896_ns<false, true>(v, t, sc, tw);
+    float2 w[32];
+    if (!dc) {
+      wave_sync();
 #pragma unroll
-    for (int k2 = 0; k2 < 32; ++k2) m[k2] = conjf2(mrow[-k2]);
-    if (dc) {  // (Z + M)/2 H(0) -> line 0, -i (Z - M)/2 H(448) -> line 448
+      for (int i = 0; i <= 16; ++i) hs[i * kR + t] = hb[i];
+      wave_sync();
+#pragma unroll
+      for (int i = 17; i < 32; ++i) hb[i] = hm[(31 - i) * kR];
+      wave_sync();
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        w[i] = cmulc(v[i], hb[i]);
+        v[i] = cmul(v[i], hb[i]);
+      }
+    } else {
       const int vn = (kHalf * kN + k1) * 8;
 #pragma unroll
+      for (int k2 = 0; k2 < 32; ++k2) w[k2] = mirror_conj896(v, k2, t, lane_base);
+#pragma unroll
       for (int k2 = 0; k2 < 32; ++k2) {
-        const float2 z = v[k2], mm = m[k2];
+        const float2 z = v[k2], mm = w[k2];
         v[k2] = cmul(make_float2(0.5f * (z.x + mm.x), 0.5f * (z.y + mm.y)), buf_ld2(rh, vh, k2 * kL * 8));
-        m[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * kL * 8));
+        w[k2] = cmul(make_float2(0.5f * (z.y - mm.y), -0.5f * (z.x - mm.x)), buf_ld2(rh, vn, k2 * kL * 8));
       }
     }
-    fft896_sn<true, kColScalar>(v, t, sc, tw);
+    fft896_sn<true, true>(v, t, sc, tw);
     {
       const int vo = (kx * kN + t) * 8;
 #pragma unroll
       for (int jj = 0; jj < kL; ++jj) buf_st2s(v[jj], rb, vo, jj * kR * 8);
     }
     if (it + 1 < kColIter) {  // next line in flight under the second inverse FFT
-      const int vo = ((kx + KSTEP) * kN + t) * 8;
 #pragma unroll
-      for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, vo, jj * kR * 8);
+      for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, lane_a + (kx + KSTEP) * kGPB * 8, jj * JSTEP);
 #pragma unroll
       for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
     }
-    fft896_sn<true, kColScalar>(m, t, sc, tw);
+    fft896_sn<true, true>(w, t, sc, tw);
     {
+      const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(Z conj H)
       const int vo = ((dc ? kHalf : kN - kx) * kN + t) * 8;
 #pragma unroll
-      for (int jj = 0; jj < kL; ++jj) buf_st2s(m[jj], rb, vo, jj * kR * 8);
+      for (int jj = 0; jj < kL; ++jj) buf_st2s(make_float2(w[jj].x, sy * w[jj].y), rb, vo, jj * kR * 8);
     }
   }
 }
@@ -404,7 +449,8 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
   if (tm) tm->begin(0, st);
-  hipLaunchKernelGGL(k_rowfwd896, dim3((unsigned)n_jobs * (P / 2) * kRB), dim3(256), 0, st, jobs, mask, pd.ws_a,
+  hipLaunchKernelGGL(k_rowfwd896, dim3((unsigned)n_jobs * (P / 2) * (kRB / kRit896)), dim3(256), 0, st, jobs, mask,
+                     pd.ws_a,
                      pd.tw, P, CH, pd.va, pd.vb);
   if (tm) tm->end(0, n_jobs, st);
   if (tm) tm->begin(1, st);
