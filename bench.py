@@ -201,9 +201,26 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
            "accepted": len(res.accepted_positions), "launches": res.launches,
            "psnr_gain_db": round(res.final_psnr - res.initial_psnr, 6),
            "full_sweep_extrapolated_s": round(CH * N * N / rate, 1),
+           "plane_cache": True,
            "note": "FFT mode, speculative first-improving batches (serial accept sequence), "
                    "prefix of the shuffled order; acceptance is highest at the start of a sweep, "
-                   "so the extrapolation is pessimistic"}
+                   "so the extrapolation is pessimistic.  Candidates propagate only the flipped "
+                   "plane's pair against the base state's cached per-plane |U|^2 (hbx_eval_flips_planes, "
+                   "the full re-propagation's PSNR bits; full_repropagation below)"}
+    # the same greedy with every candidate re-propagating all 8 planes of its group (planes=False)
+    nf = min(n_flips, 8192)
+    mf = mask.clone()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rf = dbs.greedy(plan, mf, target, order[:nf], planes=False)
+    torch.cuda.synchronize()
+    dtf = time.perf_counter() - t0
+    kpos = [p for p in res.accepted_positions if p < nf]
+    out["full_repropagation"] = {
+        "flips": rf.steps, "seconds": round(dtf, 3), "flips_per_s": round(rf.steps / dtf, 1),
+        "same_accepts_and_psnr_bits_as_plane_cache": bool(
+            rf.accepted_positions == kpos and rf.accepted_psnr == res.accepted_psnr[:len(kpos)]),
+        "note": f"first {nf} candidates of the same prefix, hbx_eval_flips (all P planes per candidate)"}
     m2 = mask.clone()
     dbs.greedy(plan, m2.clone(), target, order[:256], mode="psf")
     torch.cuda.synchronize()

@@ -372,12 +372,13 @@ int check_obs_buffers(const hbx_env_buffers_t* e) {
 // full propagation of n_ids envs (absolute ids from env_ids, or 0..n_ids-1)
 int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, const int32_t* env_ids,
                    int n_ids, float* intensity, double* chan_stats, double* psnr, const EnvDev* env,
-                   float2* field, hipStream_t st, float* plane_pool = nullptr, int32_t* plane_slot = nullptr) {
+                   float2* field, hipStream_t st, float* plane_pool = nullptr, int32_t* plane_slot = nullptr,
+                   int spares = 1) {
   const PlanDev& pd = p->pd;
-  const int CHs = pd.G * pd.P + 2;   // plane-cache slots per env
-  if (plane_pool) {                  // identity slots, then every plane's |U|^2 into its slot
+  const int CHs = pd.G * pd.P + 2 * spares;   // plane-cache slots per env
+  if (plane_pool) {                           // identity slots, then every plane's |U|^2 into its slot
     if (pd.R != 32 && pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
-    HBX_HIP(hbx::launch_plane_slot_init(env_ids, n_ids, plane_slot, pd.G * pd.P, st));
+    HBX_HIP(hbx::launch_plane_slot_init(env_ids, n_ids, plane_slot, CHs, st));
   }
   const int G = pd.G;
   const int chunk = p->max_jobs / G;
@@ -399,6 +400,7 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
     PlanDev pdx = pd;
     if (plane_pool) {
       pdx.plane_mode = hbx::kPlanesFill;
+      pdx.plane_spares = spares;
       pdx.plane_pool = env_ids ? plane_pool : plane_pool + (size_t)i0 * CHs * pd.N * pd.N;
       pdx.plane_slot = env_ids ? plane_slot : plane_slot + (size_t)i0 * CHs;
     }
@@ -787,6 +789,69 @@ int hbx_commit_flip(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, 
   const PlanDev& pd = p->pd;
   HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
                                   K, pd.G, pd.P, pd.N, pd.N, (hipStream_t)stream));
+  return HBX_OK;
+}
+
+int hbx_planes_fill(hbx_plan_t p, const uint64_t* mask, const float* target, float* plane_inten,
+                    int32_t* plane_slot, int32_t n_spare_pairs, double* chan_stats, double* psnr, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!mask || !target || !plane_inten || !plane_slot || !chan_stats)
+    return fail(HBX_ERR_INVALID, "planes fill needs mask, target, plane_inten, plane_slot and chan_stats");
+  if (n_spare_pairs < 1) return fail(HBX_ERR_INVALID, "n_spare_pairs >= 1");
+  if (p->max_jobs < p->pd.G) return fail(HBX_ERR_INVALID, "planes fill needs max_jobs >= groups");
+  HBX_HIP(hipSetDevice(p->device));
+  return propagate_full(p, mask, target, nullptr, 1, nullptr, chan_stats, psnr, nullptr, nullptr,
+                        (hipStream_t)stream, plane_inten, plane_slot, n_spare_pairs);
+}
+
+int hbx_eval_flips_planes(hbx_plan_t p, const uint64_t* base_mask, const float* target,
+                          const double* base_chan_stats, float* plane_inten, const int32_t* plane_slot,
+                          int32_t n_spare_pairs, const int64_t* flips, int32_t K, double* psnr_out,
+                          double* group_stats, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
+  if (!base_mask || !target || !base_chan_stats || !plane_inten || !plane_slot || !flips || !psnr_out)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (p->pd.R != 32 && p->pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (K > n_spare_pairs) return fail(HBX_ERR_INVALID, "K > n_spare_pairs: every candidate needs its own spare pair");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  const int N = pd.N, G = pd.G, P = pd.P, CH = G * P;
+  PlanDev pdx = pd;
+  pdx.plane_mode = hbx::kPlanesStep;
+  pdx.plane_pool = plane_inten;
+  pdx.plane_slot = plane_slot;
+  pdx.plane_spares = n_spare_pairs;   // > 1: spare pair = candidate index (1: K = 1, pair 0)
+  for (int k0 = 0; k0 < K; k0 += p->max_jobs) {
+    const int n = std::min(p->max_jobs, K - k0);
+    pdx.spare_base = k0;
+    HBX_HIP(hbx::launch_jobs_from_flips(flips + k0, n, N, N, P, CH, p->jobs, st));
+    HBX_HIP(hbx::run_jobs(pdx, p->jobs, n, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,
+                          nullptr, st));
+    HBX_HIP(hbx::launch_eval_finalize(p->jobs, pd.job_stats, n, G, base_chan_stats, psnr_out + k0,
+                                      group_stats ? group_stats + (size_t)k0 * 3 : nullptr,
+                                      pixel_count(p), p->optics.rel_scale, p->optics.peak, st));
+  }
+  return HBX_OK;
+}
+
+int hbx_commit_flip_planes(hbx_plan_t p, uint64_t* base_mask, double* base_chan_stats, double* prev_psnr,
+                           int32_t* plane_slot, int32_t n_spare_pairs, const int64_t* flips,
+                           const double* psnr_out, const double* group_stats, const int32_t* k, int32_t K,
+                           void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
+  if (!base_mask || !base_chan_stats || !prev_psnr || !plane_slot || !flips || !psnr_out || !group_stats || !k)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (K > n_spare_pairs) return fail(HBX_ERR_INVALID, "K > n_spare_pairs");
+  HBX_HIP(hipSetDevice(p->device));
+  const PlanDev& pd = p->pd;
+  HBX_HIP(hbx::launch_commit_flip(base_mask, base_chan_stats, prev_psnr, flips, psnr_out, group_stats, k,
+                                  K, pd.G, pd.P, pd.N, pd.N, (hipStream_t)stream, plane_slot));
   return HBX_OK;
 }
 

@@ -140,8 +140,11 @@ struct PlanDev {
   //                 so the group intensity is the FFT mode's bit for bit); the pair's fresh
   //                 |U|^2 go to the env's two spare slots (swapped in on accept)
   int plane_mode;
-  float* plane_pool;         // [env][CH + 2][N][N] f32 per-plane |U|^2 (env ids as the jobs carry them)
-  const int32_t* plane_slot; // [env][CH + 2] pool slot of every plane; [CH], [CH + 1] = the spares
+  float* plane_pool;         // [env][CH + 2S][N][N] f32 per-plane |U|^2 (env ids as the jobs carry them)
+  const int32_t* plane_slot; // [env][CH + 2S] pool slot of every plane; [CH + 2s], [CH + 2s + 1] = spare pair s
+  int plane_spares;          // S: spare pairs per env (0 / 1: the env step's one pair).  S > 1 (ABI v10,
+                             // hbx_eval_flips_planes): candidate j of a launch writes its pair to spare
+  int spare_base;            // pair spare_base + j, so K candidates of one base keep K fresh pairs
 };
 constexpr int kPlanesOff = 0, kPlanesFill = 1, kPlanesStep = 2;
 
@@ -273,7 +276,7 @@ hipError_t launch_eval_finalize(const JobDesc* jobs, const double* job_stats, in
                                 int rel, double peak, hipStream_t st);
 hipError_t launch_commit_flip(uint64_t* mask, double* stats, double* prev, const int64_t* flips,
                               const double* psnr, const double* gstats, const int32_t* k, int K,
-                              int G, int P, int H, int W, hipStream_t st);
+                              int G, int P, int H, int W, hipStream_t st, int32_t* plane_slot = nullptr);
 hipError_t launch_zero_record(int8_t* record, const int32_t* env_ids, int n_ids, size_t per_env,
                               hipStream_t st);
 hipError_t launch_scatter_intensity(const JobDesc* jobs, int n_jobs, const float* src, float* cache,
@@ -285,7 +288,7 @@ hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, dou
 hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
                                   size_t hw, hipStream_t st);
 // plane cache (ABI v9): slot[env][i] = i for the listed envs (env_ids nullable: 0 .. n_ids - 1)
-hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CH, hipStream_t st);
+hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CHS, hipStream_t st);
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
                            float* intensity, float* recon, int32_t* pending, int resolve, int CH, int G, size_t hw,
                            hipStream_t st);

@@ -338,7 +338,8 @@ __global__ void k_eval_finalize(const JobDesc* __restrict__ jobs, const double* 
 __global__ void k_commit_flip(uint64_t* __restrict__ mask, double* __restrict__ base_stats,
                               double* __restrict__ prev, const int64_t* __restrict__ flips,
                               const double* __restrict__ psnr, const double* __restrict__ gstats,
-                              const int32_t* __restrict__ kp, int K, int G, int P, int H, int W) {
+                              const int32_t* __restrict__ kp, int K, int G, int P, int H, int W,
+                              int32_t* __restrict__ plane_slot) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int k = *kp;
   if (k < 0 || k >= K) return;
@@ -354,6 +355,15 @@ __global__ void k_commit_flip(uint64_t* __restrict__ mask, double* __restrict__ 
   base_stats[3 * g + 1] = gstats[3 * k + 1];
   base_stats[3 * g + 2] = gstats[3 * k + 2];
   *prev = psnr[k];
+  if (plane_slot) {   // plane cache (ABI v10): candidate k's fresh pair (spare pair k) becomes current
+    const int CH = G * P, pa = g * P + ((ch % P) & ~1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int32_t cur = plane_slot[pa + i];
+      plane_slot[pa + i] = plane_slot[CH + 2 * k + i];
+      plane_slot[CH + 2 * k + i] = cur;
+    }
+  }
 }
 
 // zero record planes of reset envs
@@ -519,9 +529,9 @@ hipError_t launch_eval_finalize(const JobDesc* jobs, const double* job_stats, in
 }
 hipError_t launch_commit_flip(uint64_t* mask, double* stats, double* prev, const int64_t* flips,
                               const double* psnr, const double* gstats, const int32_t* k, int K,
-                              int G, int P, int H, int W, hipStream_t st) {
+                              int G, int P, int H, int W, hipStream_t st, int32_t* plane_slot) {
   hipLaunchKernelGGL(k_commit_flip, dim3(1), dim3(64), 0, st, mask, stats, prev, flips, psnr, gstats,
-                     k, K, G, P, H, W);
+                     k, K, G, P, H, W, plane_slot);
   return hipGetLastError();
 }
 hipError_t launch_zero_record(int8_t* record, const int32_t* env_ids, int n_ids, size_t per_env,
@@ -544,17 +554,17 @@ hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* i
 // plane cache (ABI v9): identity slots of the listed envs (the fill pass writes plane i to slot i,
 // the spares are slots CH and CH + 1)
 __global__ void k_plane_slot_init(const int32_t* __restrict__ env_ids, int n_ids, int32_t* __restrict__ slot,
-                                  int CH) {
+                                  int CHS) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_ids * (CH + 2)) return;
-  const int k = i / (CH + 2), c = i % (CH + 2);
+  if (i >= n_ids * CHS) return;
+  const int k = i / CHS, c = i % CHS;
   const int e = env_ids ? env_ids[k] : k;
-  slot[(size_t)e * (CH + 2) + c] = c;
+  slot[(size_t)e * CHS + c] = c;
 }
 
-hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CH, hipStream_t st) {
-  const int n = n_ids * (CH + 2);
-  hipLaunchKernelGGL(k_plane_slot_init, dim3((n + 255) / 256), dim3(256), 0, st, env_ids, n_ids, slot, CH);
+hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CHS, hipStream_t st) {
+  const int n = n_ids * CHS;
+  hipLaunchKernelGGL(k_plane_slot_init, dim3((n + 255) / 256), dim3(256), 0, st, env_ids, n_ids, slot, CHS);
   return hipGetLastError();
 }
 

@@ -666,7 +666,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
                                                      double* __restrict__ partial, float* __restrict__ inten_out,
                                                      float2* __restrict__ field_out, size_t tmask, int inten_by_env,
                                                      int plane_mode, float* __restrict__ plane_pool,
-                                                     const int32_t* __restrict__ plane_slot) {
+                                                     const int32_t* __restrict__ plane_slot, int plane_spares,
+                                                     int spare_base) {
   constexpr int N = R * R, GPB = 256 / R, RB = N / GPB, TL = 256 / R;
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
@@ -715,8 +716,10 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
   const PaddedScratch<R> sc{scratch + grp * R * (R + 1)};
   // plane cache (ABI v9): slots of this env's planes, pool rows of this lane group's row y
   const int CH = G * P;
-  const int32_t* slots = plane_slot ? plane_slot + (size_t)jb.env * (CH + 2) : nullptr;
-  auto pool_row = [&](int slot) { return plane_pool + (((size_t)jb.env * (CH + 2) + slot) * N + y) * N; };
+  const int CHS = CH + 2 * (plane_spares > 1 ? plane_spares : 1);   // pool slots per env
+  const int spare = CH + 2 * (plane_spares > 1 ? spare_base + j : 0);  // this job's fresh pair
+  const int32_t* slots = plane_slot ? plane_slot + (size_t)jb.env * CHS : nullptr;
+  auto pool_row = [&](int slot) { return plane_pool + (((size_t)jb.env * CHS + slot) * N + y) * N; };
   auto finish_plane = [&](pk2 (&v)[R], int p) {
     fft_group<R, true>(v, t, sc, tw);
     float f[R];
@@ -734,7 +737,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
     // go to the two spares -- the partner's bits change too (the pair is ONE complex row FFT, so
     // its rounding sees the flipped plane), which is why a step keeps both
     if (plane_mode != kPlanesOff) {
-      float* orow = pool_row(slots[plane_mode == kPlanesFill ? jb.group * P + p : CH + (p & 1)]);
+      float* orow = pool_row(slots[plane_mode == kPlanesFill ? jb.group * P + p : spare + (p & 1)]);
 #pragma unroll
       for (int k = 0; k < R; ++k) __builtin_nontemporal_store(f[k], orow + t + R * k);
     }
@@ -1045,7 +1048,8 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if constexpr (kTiledB<R>)
       hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
                          pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
-                         pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot);
+                         pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot, pd.plane_spares,
+                         pd.spare_base);
     else
       hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                          target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,

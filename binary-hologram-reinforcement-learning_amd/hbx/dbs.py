@@ -425,10 +425,15 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
            stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None,
-           graphs: bool = False) -> GreedyResult:
+           graphs: bool = False, planes: Optional[bool] = None) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
-    mode="fft": every candidate is a full propagation of its colour group.
+    mode="fft": every candidate is the FFT-mode propagation of its colour group
+    (DBS_1024_24.py:326-332).  planes (default: on at N = 1024 / 256) keeps the base
+    state's per-plane |U_p|^2 (hbx_eval_flips_planes, ABI v10): a candidate propagates
+    only its flipped plane's pair and sums the cached planes in the same order, so its
+    PSNR -- and the accept sequence -- is the full re-propagation's bit for bit;
+    planes=False re-propagates all P planes of the group per candidate.
     mode="psf": candidates are evaluated on the incremental-field path, the
     whole walk device-resident (hbx_dbs_walk_psf); the base fields are
     re-propagated exactly every ``refresh_every`` accepted flips.
@@ -448,8 +453,18 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
     total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
-    _, stats, psnr0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
-                                     stream=stream)
+    if planes is None:
+        planes = mode == "fft" and plan.cfg.height in (256, 1024)
+    if planes and (mode != "fft" or plan.cfg.height not in (256, 1024)):
+        raise ValueError("planes=True is the FFT mode's plane cache at N = 1024 / 256")
+    pool = None
+    if planes:
+        pool = plan.plane_pool(k_max)
+        stats, psnr0 = plan.planes_fill(mask, target, *pool, stream=stream)
+        stats = stats.unsqueeze(0)
+    else:
+        _, stats, psnr0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False,
+                                         stream=stream)
     base_stats = stats[0].contiguous()
     prev_dev = psnr0.clone()
     field = inten = None
@@ -474,6 +489,9 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         if mode == "psf":
             plan.eval_flips_psf(mask, target, base_stats, field, inten, flips, psnr_buf[:k], gst_buf[:k],
                                 stream=stream)
+        elif pool is not None:
+            plan.eval_flips_planes(mask, target, base_stats, *pool, flips, psnr_buf[:k], gst_buf[:k],
+                                   stream=stream)
         else:
             plan.eval_flips(mask, target, base_stats, flips, psnr_buf[:k], gst_buf[:k], stream=stream)
         launches += 1
@@ -489,6 +507,9 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         if mode == "psf":
             plan.commit_flip_psf(mask, base_stats, prev_dev, field, inten, flips, psnr_buf, gst_buf, kdev,
                                  stream=stream)
+        elif pool is not None:
+            plan.commit_flip_planes(mask, base_stats, prev_dev, *pool, flips, psnr_buf[:k], gst_buf[:k], kdev,
+                                    stream=stream)
         else:
             plan.commit_flip(mask, base_stats, prev_dev, flips, psnr_buf, gst_buf, kdev, stream=stream)
         prev = float(ps[i])

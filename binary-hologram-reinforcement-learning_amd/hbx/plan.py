@@ -293,6 +293,66 @@ class Plan:
                                            _stream(stream)), "hbx_eval_flips")
         return psnr_out, group_stats
 
+    # -- plane-cached candidates (ABI v10): the FFT mode's bits, only the flipped pair propagated
+    def plane_pool(self, spare_pairs: int):
+        """(plane_inten f32 [CH + 2 S, H, W], plane_slot int32 [CH + 2 S]) for one base env."""
+        c = self.cfg
+        n = c.channels + 2 * int(spare_pairs)
+        return (torch.empty((n, c.height, c.width), dtype=torch.float32, device=self.device),
+                torch.empty((n,), dtype=torch.int32, device=self.device))
+
+    def _check_pool(self, plane_inten, plane_slot):
+        c = self.cfg
+        n = plane_slot.shape[0] if isinstance(plane_slot, torch.Tensor) else -1
+        _need(plane_slot, "plane_slot", torch.int32, (n,), self.device)
+        _need(plane_inten, "plane_inten", torch.float32, (n, c.height, c.width), self.device)
+        if n < c.channels + 2 or (n - c.channels) % 2:
+            raise ValueError(f"plane pool of {n} slots: need CH + 2 S with S >= 1")
+        return (n - c.channels) // 2
+
+    def planes_fill(self, mask, target, plane_inten, plane_slot, stream=None):
+        """Full propagation of ONE base env into its plane pool (hbx_planes_fill):
+        returns (chan_stats f64 [G, 3], psnr f64 [1])."""
+        c = self.cfg
+        _need(mask, "mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        s = self._check_pool(plane_inten, plane_slot)
+        stats = torch.empty((c.groups, 3), dtype=torch.float64, device=self.device)
+        psnr = torch.empty((1,), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_planes_fill(self._h, _ptr(mask), _ptr(target), _ptr(plane_inten), _ptr(plane_slot),
+                                            s, _ptr(stats), _ptr(psnr), _stream(stream)), "hbx_planes_fill")
+        return stats, psnr
+
+    def eval_flips_planes(self, base_mask, target, base_stats, plane_inten, plane_slot, flips,
+                          psnr_out=None, group_stats=None, stream=None):
+        """eval_flips with the base env's plane pool: the same PSNRs bit for bit."""
+        c = self.cfg
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
+        s = self._check_pool(plane_inten, plane_slot)
+        k = flips.shape[0]
+        _need(flips, "flips", torch.int64, (k,), self.device)
+        if psnr_out is None:
+            psnr_out = torch.empty((k,), dtype=torch.float64, device=self.device)
+        if group_stats is None:
+            group_stats = torch.empty((k, 3), dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.hbx_eval_flips_planes(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                                  _ptr(plane_inten), _ptr(plane_slot), s, _ptr(flips), k,
+                                                  _ptr(psnr_out), _ptr(group_stats), _stream(stream)),
+                   "hbx_eval_flips_planes")
+        return psnr_out, group_stats
+
+    def commit_flip_planes(self, base_mask, base_stats, prev_psnr, plane_inten, plane_slot, flips, psnr_out,
+                           group_stats, k_dev: torch.Tensor, stream=None):
+        """Commit candidate k_dev of an eval_flips_planes batch (its fresh pair swaps in)."""
+        k = self._check_commit(base_mask, base_stats, prev_psnr, flips, psnr_out, group_stats, k_dev)
+        s = self._check_pool(plane_inten, plane_slot)
+        _lib.check(self.lib.hbx_commit_flip_planes(self._h, _ptr(base_mask), _ptr(base_stats), _ptr(prev_psnr),
+                                                   _ptr(plane_slot), s, _ptr(flips), _ptr(psnr_out),
+                                                   _ptr(group_stats), _ptr(k_dev), k, _stream(stream)),
+                   "hbx_commit_flip_planes")
+
     def eval_flips_psf(self, base_mask, target, base_stats, field, intensity, flips,
                        psnr_out=None, group_stats=None, stream=None):
         """eval_flips on the incremental-field path: field [CH, H, W, 2] f32 and

@@ -256,6 +256,31 @@ int hbx_commit_flip(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stat
                     double* prev_psnr, const int64_t* flips, const double* psnr_out,
                     const double* group_stats, const int32_t* k, int32_t K, void* stream);
 
+/* (ABI v10) hbx_eval_flips / hbx_commit_flip with the base env's per-plane
+ * |U_p|^2 cached (N = 1024 / 256): the speculative greedy DBS of
+ * DBS_1024_24.py:313-363 in the FFT mode, bit for bit, at a fraction of the
+ * bytes.  A candidate flips one plane, so only that plane's PAIR (the two
+ * planes one complex row FFT carries) is propagated; the group intensity sums
+ * the cached planes and the pair's fresh ones in the FFT mode's plane order,
+ * i.e. the same f32 sum.  Candidate k writes its pair's fresh |U|^2 to spare
+ * pair k of the pool; committing candidate k swaps that pair's slots in.
+ *   plane_inten [CH + 2 S][H][W] f32, plane_slot [CH + 2 S] int32 (S =
+ *   n_spare_pairs >= K): filled by hbx_planes_fill from the base mask
+ *   (identity slots, every plane's |U|^2, the base chan_stats / psnr).
+ * Replaces the per-flip tt.simulate of the whole colour group
+ * (DBS_1024_24.py:326-332) in speculative batches. */
+int hbx_planes_fill(hbx_plan_t plan, const uint64_t* mask, const float* target, float* plane_inten,
+                    int32_t* plane_slot, int32_t n_spare_pairs, double* chan_stats, double* psnr,
+                    void* stream);
+int hbx_eval_flips_planes(hbx_plan_t plan, const uint64_t* base_mask, const float* target,
+                          const double* base_chan_stats, float* plane_inten, const int32_t* plane_slot,
+                          int32_t n_spare_pairs, const int64_t* flips, int32_t K, double* psnr_out,
+                          double* group_stats, void* stream);
+int hbx_commit_flip_planes(hbx_plan_t plan, uint64_t* base_mask, double* base_chan_stats,
+                           double* prev_psnr, int32_t* plane_slot, int32_t n_spare_pairs,
+                           const int64_t* flips, const double* psnr_out, const double* group_stats,
+                           const int32_t* k, int32_t K, void* stream);
+
 /* hbx_eval_flips / hbx_commit_flip on the incremental-field path: the base
  * env additionally carries its per-plane field [CH][H][W][2] and group
  * intensities [G][H][W] (hbx_simulate), so a candidate costs one streaming

@@ -1,6 +1,6 @@
 """The drop-in env classes (hbx.env.BinaryHologramEnv / Group / MD) under the
-reference's own contracts, and the literal DBS_1024_24.py driver statements
-running against them through the torchOptics shim.
+reference's own contracts, and a builder-written driver with DBS_1024_24.py's
+contract (not its text) running against them through the torchOptics shim.
 
 Reference contracts checked:
   env.py:42-52      observation_space Dict / Discrete action_space

@@ -185,6 +185,33 @@ def test_fft_greedy_1024x24_vs_oracle(golden_dir, name):
     plan.close()
 
 
+@pytest.mark.parametrize("name,stop", [("dbs_prefix_1024x24_16k.npz", None), ("dbs_ratio05_256.npz", 0.5),
+                                       ("dbs_prefix_1024x24_phase.npz", None)])
+def test_fft_greedy_plane_cache_equals_full_repropagation(golden_dir, name, stop):
+    """the FFT-mode greedy with the base state's plane cache (hbx_eval_flips_planes,
+    only the flipped plane's pair propagated per candidate) makes the full re-propagation's
+    decisions with the full re-propagation's PSNR BITS -- every accepted PSNR equal, the same
+    candidates visited, the same final mask."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, name)
+    n = int(d["n"])
+    runs = {}
+    for planes in (False, True):
+        plan, mask, target = _dev(ocfg, pre, tgt)
+        res = dbs.greedy(plan, mask, target, order[:n], stop_diff=stop, mode="fft", planes=planes)
+        runs[planes] = (res, mask.cpu().numpy())
+        plan.close()
+    (full, m_full), (cached, m_cached) = runs[False], runs[True]
+    print(f"{name}: {cached.steps} candidates, {len(cached.accepted_positions)} accepts, "
+          f"{cached.launches} batches")
+    assert cached.accepted_positions == full.accepted_positions
+    assert cached.accepted_psnr == full.accepted_psnr                 # bit for bit
+    assert cached.initial_psnr == full.initial_psnr and cached.final_psnr == full.final_psnr
+    assert cached.steps == full.steps and cached.stopped_early == full.stopped_early
+    assert np.array_equal(m_full, m_cached)
+    assert len(cached.accepted_positions) > 100
+
+
 def test_candidate_change_precision_1024x24(golden_dir):
     """Each candidate's PSNR change against the initial state, accepted or not
     (probe sweep / speculative batches): incremental path within INCR_TOL_DB,

@@ -127,7 +127,45 @@ def col2_stage_conflicts(R, pos):
     return rd16, rd32, wr
 
 
+def tile896_pos(kx, r):
+    """hbx_passes896.hip tile896_pos (r04): k_rowfwd896's plane tile [kx < 448][8 rows]."""
+    m = kx % 28
+    return kx * 8 + (r ^ ((((m >> 2) & 7) ^ (((m >> 1) & 1) * 5)) & 7))
+
+
+def tile_pos_32_8(line, r):
+    """hbx_rowcol.hpp tile_pos<32, 8> (the r01-r03 k_rowfwd896 tile)."""
+    return line * 8 + (r ^ ((((line & 31) >> 2) ^ (((line >> 1) & 1) * 5)) & 7))
+
+
+def rowfwd896_tile_conflicts(pos):
+    """Extra bank cycles of k_rowfwd896's plane tile per row block and plane: (lane-row writes
+    kx = t + 28 k2 as ds_write_b64, 16-B chunk reads as ds_read_b64, the same as 16-lane reads)."""
+    G16 = [range(i * 16, (i + 1) * 16) for i in range(4)]
+    G32 = [range(0, 32), range(32, 64)]
+    wr = rd64 = rd16 = 0
+    for w in range(4):
+        for k2 in range(16):
+            addrs = []
+            for lane in range(64):
+                grp, t = w * 2 + lane // 32, lane % 32
+                addrs.append(2 * pos(t + 28 * k2, grp) if t < 28 else None)
+            live = [a for a in addrs if a is not None]
+            wr += _extra([a if a is not None else live[0] for a in addrs], G16, 32)
+        for i in range(7):
+            for half in (0, 1):
+                addrs = []
+                for lane in range(64):
+                    c = w * 64 + lane + 256 * i
+                    addrs.append(2 * pos(c // 4, (c % 4) * 2 + half))
+                rd64 += _extra(addrs, G32, 64)
+                rd16 += _extra(addrs, G16, 32)
+    return wr, rd64, rd16
+
+
 if __name__ == "__main__":
+    print("k_rowfwd896 tile (write, read_b64, read2): tile_pos<32, 8>", rowfwd896_tile_conflicts(tile_pos_32_8),
+          "tile896_pos", rowfwd896_tile_conflicts(tile896_pos))
     for R in (32, 16):
         print(f"k_col2 R={R} stage (read2 16-lane, read_b64 32-lane, write): r03",
               col2_stage_conflicts(R, col2_pos_r03), "r04", col2_stage_conflicts(R, col2_pos))
