@@ -40,3 +40,13 @@ def test_r04_placement_is_a_bijection_inside_each_region():
         for sp in range(TL // 2):
             pos = [M.col2_pos(R, sp, y) for y in range(N)]
             assert len(set(pos)) == N and min(pos) >= 0 and max(pos) < RS, (R, sp)
+
+
+def test_rowfwd896_tile_keyed_on_kx_mod_28():
+    """r04 k_rowfwd896: the tile swizzle keyed on kx mod 28 (one lane base for the lane-row
+    writes kx = t + 28 k2) loses tile_pos<32, 8>'s write conflicts and keeps the 16-lane
+    chunk reads conflict-free."""
+    import lds_swizzle_model as M
+    wr, rd64, rd16 = M.rowfwd896_tile_conflicts(M.tile896_pos)
+    wr0, _, _ = M.rowfwd896_tile_conflicts(M.tile_pos_32_8)
+    assert wr == 0 and rd16 == 0 and rd64 <= 16 and wr0 > 0

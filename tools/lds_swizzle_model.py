@@ -87,13 +87,16 @@ def col2_pos(R, sp, y):
 
 
 def _extra(addrs, groups, mod):
+    """Extra cycles: per lane group, the busiest bank's distinct addresses minus one (None = an
+    inactive lane, EXEC off)."""
     tot = 0
     for g in groups:
         banks = {}
         for lane in g:
             a = addrs[lane]
-            banks.setdefault(a % mod, set()).add(a)
-        tot += max(len(v) for v in banks.values()) - 1
+            if a is not None:
+                banks.setdefault(a % mod, set()).add(a)
+        tot += max((len(v) for v in banks.values()), default=1) - 1
     return tot
 
 
@@ -150,8 +153,7 @@ def rowfwd896_tile_conflicts(pos):
             for lane in range(64):
                 grp, t = w * 2 + lane // 32, lane % 32
                 addrs.append(2 * pos(t + 28 * k2, grp) if t < 28 else None)
-            live = [a for a in addrs if a is not None]
-            wr += _extra([a if a is not None else live[0] for a in addrs], G16, 32)
+            wr += _extra(addrs, G16, 32)
         for i in range(7):
             for half in (0, 1):
                 addrs = []

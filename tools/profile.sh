@@ -7,7 +7,7 @@ TAG=${1:-run}; shift
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="python3 bench.py --steps 6 --warmup 2 --psf-steps 20 --cpu-sample 0 --dbs-flips 0 --no-probe --no-psnr-check --no-precision --no-planes $*"
+BENCH="python3 bench.py --steps 6 --warmup 2 --psf-steps 20 --cpu-sample 0 --dbs-flips 0 --no-probe --no-psnr-check --no-precision --no-planes --no-crop --no-obs $*"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BENCH > $OUT/trace.log 2>&1 || exit 1
 # headline-only trace: every FFT-mode pass launch is a 128-job step / reset chunk, so the
 # --stats average of the dominant kernel is directly comparable with bench.py's roofline
