@@ -578,9 +578,12 @@ __device__ __forceinline__ void dft28_pk(float2 (&v)[32]) {
 // 896-point FFT by 32 lanes, natural layout in -> slot layout out.
 // tw896: LDS [k1 < 28][t < 32] = W896^{t k1} (forward sign); INV conjugates.
 // SCALAR: scalar-f32 32-point DFTs (fewer live registers than the packed ones
-// when a kernel keeps two lines in flight)
-template <bool INV, bool SCALAR = false, class Scratch>
-__device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+// when a kernel keeps two lines in flight).  _s1 = the 28-point DFTs and twiddles
+// (registers and the twiddle table only), _s2 = the transpose through the group's
+// scratch and the 32-point DFTs: a kernel that shares the scratch can sit a block
+// barrier between them (k_col896).
+template <bool INV, bool SCALAR = false>
+__device__ __forceinline__ void fft896_ns_s1(float2 (&v)[32], int t, const float2* tw896) {
   asm volatile("" ::: "memory");
   if constexpr (SCALAR) {
     dft28<INV>(v);
@@ -597,6 +600,9 @@ __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch&
       v[k1] = from_pk(INV ? pk_cmulc(to_pk(v[k1]), w) : pk_cmul(to_pk(v[k1]), w));
     }
   }
+}
+template <bool INV, bool SCALAR = false, class Scratch>
+__device__ __forceinline__ void fft896_ns_s2(float2 (&v)[32], int t, const Scratch& sc) {
   wave_sync();
 #pragma unroll
   for (int k1 = 0; k1 < 28; ++k1) *sc.at(t, k1) = v[k1];
@@ -608,6 +614,11 @@ __device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch&
   wave_sync();
   if constexpr (SCALAR) dft_reg_scalar<32, INV>(v);
   else dft_reg<32, INV>(v);
+}
+template <bool INV, bool SCALAR = false, class Scratch>
+__device__ __forceinline__ void fft896_ns(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+  fft896_ns_s1<INV, SCALAR>(v, t, tw896);
+  fft896_ns_s2<INV, SCALAR>(v, t, sc);
 }
 
 // fft896_ns with half the scratch (r04, k_rowfwd896 at three workgroups per CU): the transpose
@@ -640,12 +651,16 @@ __device__ __forceinline__ void fft896_ns_split(float2 (&v)[32], int t, float* s
 }
 
 // 896-point FFT by 32 lanes, slot layout in -> natural layout out (adjoint of
-// fft896_ns: the same stages in reverse order with the opposite sign)
-template <bool INV, bool SCALAR = false, class Scratch>
-__device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+// fft896_ns: the same stages in reverse order with the opposite sign); _s1 = the
+// 32-point DFTs in registers, _s2 = transpose, twiddles, 28-point DFTs
+template <bool INV, bool SCALAR = false>
+__device__ __forceinline__ void fft896_sn_s1(float2 (&v)[32]) {
   asm volatile("" ::: "memory");
   if constexpr (SCALAR) dft_reg_scalar<32, INV>(v);   // over k2 -> index t (the natural lane)
   else dft_reg<32, INV>(v);
+}
+template <bool INV, bool SCALAR = false, class Scratch>
+__device__ __forceinline__ void fft896_sn_s2(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
   wave_sync();
   // lane k1 (< 28) holds B[k1][t] for t = 0..31 in v[t]
   if (t < 28) {
@@ -671,6 +686,11 @@ __device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch&
     }
     dft28_pk<INV>(v);
   }
+}
+template <bool INV, bool SCALAR = false, class Scratch>
+__device__ __forceinline__ void fft896_sn(float2 (&v)[32], int t, const Scratch& sc, const float2* tw896) {
+  fft896_sn_s1<INV, SCALAR>(v);
+  fft896_sn_s2<INV, SCALAR>(v, t, sc, tw896);
 }
 
 }  // namespace hbx

@@ -94,7 +94,6 @@ struct TileB {
 };
 template <int R>
 constexpr bool kTiledB = R == 32 || R == 16;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // Pass 1
@@ -110,7 +109,7 @@ template <int R>
 constexpr int rowfwd_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }   // N = 256: 2 (r03,
 // with nt A stores: 0.0634 -> 0.0585 ms; 4 row blocks 0.0611)
 
-template <int R, int NT, int SK>
+template <int R, int NT, int SK, int RIT = rowfwd_iters<R>()>
 __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
                                                    const uint32_t* __restrict__ mask,
                                                    float2* __restrict__ ws_a,
@@ -120,7 +119,6 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   constexpr int GPB = NT / R;          // rows per row block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
   constexpr int SCR = GPB * R * (R + 1);
-  constexpr int RIT = rowfwd_iters<R>();
   static_assert(N * GPB <= SCR, "tile must fit in the scratch area");
   __shared__ float2 tw[N];
   __shared__ __attribute__((aligned(16))) float2 lds[SCR];
@@ -241,7 +239,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
 //    group (fft_group_split), and the Hermitian split goes out one plane at a time
 //    through a 32-KB tile that aliases those FFT tiles: 8 KB twiddles + 33.8 KB.
 // Same arithmetic as k_rowfwd, so the A it writes is bit-identical.
-template <int SK>
+template <int SK, int RIT = rowfwd_iters<32>()>
 __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__ jobs,
                                                      const uint32_t* __restrict__ mask,
                                                      float2* __restrict__ ws_a,
@@ -250,7 +248,6 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
   constexpr int R = 32, NT = 256, N = R * R;
   constexpr int GPB = NT / R;          // 8 rows per row block
   constexpr int WPR = N / 32;          // 32 mask words per row = one per lane
-  constexpr int RIT = rowfwd_iters<R>();
   constexpr int SCRF = GPB * R * (R + 1);               // floats: 8 FFT tiles
   static_assert((N / 2) * GPB * 2 <= SCRF, "one plane's tile must fit in the FFT tiles");
   __shared__ float2 tw[N];
@@ -384,29 +381,6 @@ __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ?
 // is done with it; no block barrier), row y at col2_pos(g / 2, y).  After a block barrier,
 // col2_stage_store: the block stores the set as 16-B chunks (slots 2 sp, 2 sp + 1 from
 // regions 2 sp, 2 sp + 1) in memory order -- one contiguous run per 16-row band.
-template <int R>
-constexpr int col2_region_stride() { return R * (R + 1) > R * R + 32 ? R * (R + 1) : R * R + 32; }
-template <int R>
-__device__ __forceinline__ float2* col2_region(float2* scratch, int g) {
-  return scratch + g * col2_region_stride<R>();
-}
-// Where row y of slot pair sp's regions sits.  The readers (col2_stage_store) load the rows
-// y0 = band * 16 + (tid / NSP) % 16 of the NSP = TL / 2 slot pairs sp = tid % NSP; gfx950 serves
-// the compiler's ds_read2(st64)_b64 as 16-lane groups over 32 banks (16 float2: NSP pairs x
-// 16 / NSP rows) and a ds_read_b64 as 32-lane groups over 64 banks (NSP pairs x 32 / NSP rows).
-// A constant shift per pair cannot serve both (r03's (sp * 64 / TL) was the 64-bank one; the
-// compiler emits read2st64, and rocprofv3 counted 67.1 M SQ_LDS_BANK_CONFLICT cycles per 128-job
-// k_col2 launch = 8 extra cycles on each of the 32 stage reads per wave and line).  Shift sp by
-// 32 / TL float2 and flip row bit 4 (+16 banks) when row bit HB (the bit splitting a 32-lane
-// group's rows in halves) is set, except for the last pair: conflict-free in both models, and
-// the writers' 16-lane runs of consecutive rows stay conflict-free (tools/lds_swizzle_model.py
-// checks all three; found by exhaustive search over this family).
-template <int R>
-__device__ __forceinline__ int col2_pos(int sp, int y) {
-  constexpr int TL = 256 / R, NSP = TL / 2, HB = ilog2c(16 / NSP);
-  return sp * (32 / TL) + (y ^ ((((y >> HB) & 1) && sp != NSP - 1) ? 16 : 0));
-}
-
 template <int R, int SK>
 __device__ __forceinline__ void col2_stage_write(const float2 (&v)[R], float sy, float2* scratch, int grp, int t) {
   // row y = t + R k2: col2_pos only touches bits < 5, so rows R q apart with R q a multiple of
@@ -423,38 +397,7 @@ __device__ __forceinline__ void col2_stage_write(const float2 (&v)[R], float sy,
   }
 }
 
-template <int R>
-__device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
-  constexpr int N = R * R, TL = 256 / R, CH = N * TL / 2;   // 16-B chunks per line set
-  // chunk c = tid + 256 i: band c / (8 TL) = tid / (8 TL) + (32 / TL) i, row (tid / (TL / 2)) % 16,
-  // slot pair tid % (TL / 2); memory offset = lane part + i (32 / TL) 16 N + st 16 TL (soffset)
-  const int tid = threadIdx.x, sp = tid % (TL / 2);
-  const int band0 = tid / (8 * TL), r = (tid / (TL / 2)) % 16;
-  const int y0 = band0 * 16 + r;
-  // rows y0 + (32 / TL) 16 i differ from y0 in bits >= 5 only, so col2_pos moves with them
-  static_assert((32 / TL) * 16 >= 32, "stage rows step past the swizzled bits");
-  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + col2_pos<R>(sp, y0);
-  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + col2_pos<R>(sp, y0);
-  const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
-#pragma unroll
-  for (int i = 0; i < CH / 256; ++i) {
-    const float2 lo = lo_r[(32 / TL) * 16 * i];   // (rounded by col2_stage_write under SK)
-    const float2 hi = hi_r[(32 / TL) * 16 * i];
-    const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
-    // non-temporal (nt): B streams out without taking Infinity-Cache residency, so its write-back
-    // no longer lands on top of k_rowinv's reads (r03: N = 256 k_col2 0.143 -> 0.128 ms and
-    // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419).
-    // soffset stays the literal 0, the whole offset rides in voffset: LLVM's gfx950 hazard
-    // recognizer inserts the 2 wait states a VALU write of a >64-bit store's data VGPRs needs
-    // only when the MUBUF soffset is not a register -- with an SGPR soffset (r03) it assumed no
-    // hazard and scheduled such writes right behind the store, the cause of the r03 bf16
-    // non-determinism and of the ITER = 1 wrong B rows (tools/hazard_scan.py
-    // now rejects any wide buffer store with a register soffset)
-    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff + (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, 0, kBufNT);
-  }
-}
-
-template <int R, int SK>
+template <int R, int SK, int ITER = col2_iters<R>()>
 __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ jobs,
                                                  const float2* __restrict__ ws_a,
                                                  float2* __restrict__ ws_b,
@@ -463,7 +406,6 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
                                                  int pair_step) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // lane groups (= input lines) per block iteration
-  constexpr int ITER = col2_iters<R>();
   constexpr int LB = (N / 2) / (GPB * ITER);
   static_assert((N / 2) % (GPB * ITER) == 0, "line blocking");
   __shared__ float2 tw[N];
@@ -1023,23 +965,50 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   PassTimer* tm = pd.timer;
   const int pair = pd.plane_mode == kPlanesStep ? 1 : 0;
   if (pd.plane_mode != kPlanesOff && (!kTiledB<R> || !pd.plane_pool || !pd.plane_slot)) return hipErrorInvalidValue;
+  // Small batches (greedy DBS, a few candidates per launch): the walk-per-workgroup loops
+  // (rowfwd_iters row blocks, col2_iters lines) trade parallelism for store overlap, which pays
+  // only when the launch fills the chip many times over.  Below kSmallBlocks workgroups the
+  // launch runs one row block / one line per workgroup instead -- the same arithmetic, so
+  // bit-identical results (tests/test_gpu_dbs_headline.py plane-cache / full re-propagation).
+  constexpr unsigned kSmallBlocks = 2048;
+  const unsigned rf_blocks = (unsigned)n_jobs * (pair ? 1 : P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
+  const unsigned col_blocks = (unsigned)n_jobs * (pair ? 2 : P) * ((N / 2) / (GPB * col2_iters<R>()));
+  const bool small = kTiledB<R> && rf_blocks < kSmallBlocks && col_blocks < kSmallBlocks;
   {
-    const unsigned blocks = (unsigned)n_jobs * (pair ? 1 : P / 2) * (N / (kRowNT<R> / R)) / rowfwd_iters<R>();
     if (tm) tm->begin(0, st);
-    if constexpr (R == 32)
-      hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
-                         pd.va, pd.vb, pair);
-    else
-    hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a, pd.tw, P,
-                       CH, pd.va, pd.vb, pair);
+    if constexpr (R == 32) {
+      if (small)
+        hipLaunchKernelGGL((k_rowfwd32<SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(256), 0, st, jobs, mask,
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+      else
+        hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(rf_blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
+                           pd.va, pd.vb, pair);
+    } else if constexpr (kTiledB<R>) {
+      if (small)
+        hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(kRowNT<R>), 0,
+                           st, jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+      else
+        hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask,
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+    } else {
+      hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a,
+                         pd.tw, P, CH, pd.va, pd.vb, pair);
+    }
     if (tm) tm->end(0, n_jobs, st);
   }
   {
     if (tm) tm->begin(1, st);
-    constexpr int LINES_PER_BLOCK = GPB * col2_iters<R>();
-    const unsigned blocks = (unsigned)n_jobs * (pair ? 2 : P) * ((N / 2) / LINES_PER_BLOCK);
-    hipLaunchKernelGGL((k_col2<R, SK>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab, pd.tw, P,
-                       pair);
+    if constexpr (kTiledB<R>) {
+      if (small)
+        hipLaunchKernelGGL((k_col2<R, SK, 1>), dim3(col_blocks * col2_iters<R>()), dim3(256), 0, st, jobs, pd.ws_a,
+                           pd.ws_b, pd.htab, pd.tw, P, pair);
+      else
+        hipLaunchKernelGGL((k_col2<R, SK>), dim3(col_blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
+                           pd.tw, P, pair);
+    } else {
+      hipLaunchKernelGGL((k_col2<R, SK>), dim3(col_blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
+                         pd.tw, P, pair);
+    }
     if (tm) tm->end(1, n_jobs, st);
   }
   {

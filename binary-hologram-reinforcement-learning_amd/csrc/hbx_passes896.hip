@@ -205,10 +205,18 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
 // 4-MB L2 instead of the whole 3.2-MB table (r03: 1.22x the algorithmic bytes, the H rows
 // re-fetched across jobs of different colour groups).
 // ---------------------------------------------------------------------------
-constexpr bool kInvScalar = false;   // k_rowinv896: packed DFTs (one line live)
 constexpr int kColIter = 7;
 constexpr int kColLB = kHalf / (kGPB * kColIter);   // 8 line blocks per plane = one per XCD
 static_assert(kHalf % (kGPB * kColIter) == 0 && kColLB == 8, "line blocking");
+
+// each group writes its output line (natural layout: lane t, register j -> row t + 32 j) into its
+// own scratch region at col2_pos (hbx_rowcol.hpp); rows 32 apart share a lane base
+__device__ __forceinline__ void col896_stage_write(const float2 (&v)[32], float sy, float2* scratch, int grp,
+                                                   int t) {
+  float2* base = col2_region<kR>(scratch, grp) + col2_pos<kR>(grp >> 1, t);
+#pragma unroll
+  for (int jj = 0; jj < kL; ++jj) base[kR * jj] = make_float2(v[jj].x, sy * v[jj].y);
+}
 
 __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ jobs,
                                                    const float2* __restrict__ ws_a,
@@ -233,6 +241,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * kPlaneB, (unsigned)(kPlaneB * 8));
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (kHalf + 1) * kN,
                                                (unsigned)((kHalf + 1) * kN * 8));
+  static_assert(col2_region_stride<kR>() == kR * (kR + 1), "stage regions are the FFT scratch regions");
   float2* const hs = scratch + grp * kR * (kR + 1);
   const PaddedScratch<kR> sc{hs};
   const int k1 = t < kL ? t : 0;   // slot lane (28..31 carry don't-care values)
@@ -258,11 +267,13 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     const bool dc = (kx == 0);
     const int vh = (kx * kN + k1) * 8;   // H(kx, ky = k1 + 28 k2) at vh + k2 * 28 * 8
     float2 hb[32];
-    if (!dc) {
+    fft896_ns_s1<false, true>(v, t, tw);
+    if (!dc) {   // H(kx, ky <= 448), in flight under the transpose
 #pragma unroll
       for (int i = 0; i <= 16; ++i) hb[i] = buf_ld2(rh, vh, i * kL * 8);
     }
-    fft896_ns<false, true>(v, t, sc, tw);
+    if (it > 0) lds_barrier();   // the previous iteration's second set has been read out
+    fft896_ns_s2<false, true>(v, t, sc);
     float2 w[32];
     if (!dc) {
       wave_sync();
@@ -289,30 +300,41 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
       }
     }
     fft896_sn<true, true>(v, t, sc, tw);
-    {
-      const int vo = (kx * kN + t) * 8;
-#pragma unroll
-      for (int jj = 0; jj < kL; ++jj) buf_st2s(v[jj], rb, vo, jj * kR * 8);
-    }
+    // B in 1-KB slot tiles (r04, as N = 1024): the block's 8 lines kxb .. kxb + 7 are slot tile
+    // kxb / 8; their mirrors N - kx (448 for kx = 0) are slots 448 + kx, tile 56 + kxb / 8
+    const int kxb = kx - grp;
+    col896_stage_write(v, 1.0f, scratch, grp, t);
+    lds_barrier();
+    col2_stage_store<kR, kN>(scratch, rb, kxb / kGPB);
     if (it + 1 < kColIter) {  // next line in flight under the second inverse FFT
 #pragma unroll
       for (int jj = 0; jj < kL; ++jj) v[jj] = buf_ld2s(ra, lane_a + (kx + KSTEP) * kGPB * 8, jj * JSTEP);
 #pragma unroll
       for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
     }
-    fft896_sn<true, true>(w, t, sc, tw);
-    {
-      const float sy = dc ? 1.0f : -1.0f;   // line N - kx = conj IFFT(Z conj H)
-      const int vo = ((dc ? kHalf : kN - kx) * kN + t) * 8;
-#pragma unroll
-      for (int jj = 0; jj < kL; ++jj) buf_st2s(make_float2(w[jj].x, sy * w[jj].y), rb, vo, jj * kR * 8);
-    }
+    fft896_sn_s1<true, true>(w);
+    lds_barrier();   // the first set has been read out: the regions are the FFTs' again
+    fft896_sn_s2<true, true>(w, t, sc, tw);
+    col896_stage_write(w, dc ? 1.0f : -1.0f, scratch, grp, t);   // line N - kx = conj IFFT(Z conj H)
+    lds_barrier();
+    col2_stage_store<kR, kN>(scratch, rb, (kHalf + kxb) / kGPB);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pass 3
+// Pass 3 (r04: k_rowinv_d's scheme at 896): 8 rows per block, all P planes; every lane loads
+// its own FFT input straight from B's slot tiles -- no LDS tile, no block barrier in the plane
+// loop (r01-r03: an LDS tile transpose of 64-B line pieces between three block barriers per
+// plane, 0.56-0.59 of 8 TB/s).  The group for row y needs, in slot layout, lane k1 < 28 and
+// register k2 < 32: kx = k1 + 28 k2, i.e. slot s = kx (kx <= 448) or 1344 - kx (kx > 448):
+//   k2 = 2 m + b < 16:          s = 28 b + k1 + 56 m        -> lane base lo[b] + m * 7 tiles
+//   k2 = 31 - (2 m + b) > 16:   s = 476 - k1 + 28 b + 56 m  -> lane base hi[b] + m * 7 tiles
+//   k2 = 16:                    lane 0: s = 448 (Nyquist line), lanes k1 > 0: hi[1] + 7 * 7 tiles
+// (56 slots = 7 whole 8-slot tiles, so every offset is the lane base plus a constant).  Eight
+// consecutive lanes read a 64-B tile row; a wave's two rows are adjacent: 128 B.
 // ---------------------------------------------------------------------------
+constexpr bool kInvScalar = false;   // packed DFTs (one line live)
+
 __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict__ jobs,
                                                       const float2* __restrict__ ws_b,
                                                       const float* __restrict__ target,
@@ -321,12 +343,9 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
                                                       float* __restrict__ inten_out,
                                                       float2* __restrict__ field_out, size_t tmask,
                                                       int inten_by_env) {
-  constexpr int CH16 = kN * kGPB / 2;   // 16-B chunks per plane tile
-  constexpr int PER = CH16 / 256;
-  static_assert(CH16 % 256 == 0, "chunking");
-  constexpr int PF = 8 < PER ? 8 : PER;   // chunks prefetched a plane ahead (all of them spilled)
+  constexpr int TL = 8;                           // slots per tile (1-KB tiles, as N = 1024)
   __shared__ float2 tw[kN];
-  __shared__ __attribute__((aligned(16))) float2 tile[kSCR];
+  __shared__ float2 scratch[kSCR];
   __shared__ double red[kGPB][3];
   for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
 
@@ -343,60 +362,37 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
     }
     return;
   }
-  const int y0 = rb * kGPB;
-  const int y = y0 + grp;
-  const float2* jbase = ws_b + (size_t)j * P * kPlaneB;
-  const int k1 = t < kL ? t : 0;
-
-  // this thread's share of a plane tile: PF chunks prefetched one plane ahead
-  // in registers, the rest loaded when the tile is written (register budget)
-  float4 pre[PF];
+  const int y = rb * kGPB + grp;
+  const __amdgpu_buffer_rsrc_t rs = plane_rsrc(ws_b + (size_t)j * P * kPlaneB, (unsigned)((size_t)P * kPlaneB * 8));
+  const int k1 = t < kL ? t : 0;                  // lanes 28..31 mirror lane 0 (don't-care values)
+  const int yb = (y >> 4) * 16 * kN + (y & 15) * TL;
+  auto at = [&](int slot) { return (yb + (slot / TL) * 16 * TL + slot % TL) * 8; };   // bytes
+  const int lo0 = at(k1), lo1 = at(28 + k1);
+  const int hi0 = at(476 - k1), hi1 = at(504 - k1);
+  constexpr int MS = 7 * 16 * TL * 8;             // bytes per m: 7 tiles
+  const int mid = k1 == 0 ? at(kHalf) : hi1 + 7 * MS;
+  auto load_plane = [&](float2 (&v)[32], int p) {
+    const int po = p * (int)(kPlaneB * 8);
 #pragma unroll
-  for (int i = 0; i < PF; ++i) {
-    const int c = threadIdx.x + 256 * i;
-    const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-    pre[i] = ld_stream4(jbase + (size_t)line * kN + y0 + r2);
-  }
+    for (int k2 = 0; k2 < 32; ++k2) {
+      if (k2 < 16) v[k2] = buf_ld2s(rs, (k2 & 1) ? lo1 : lo0, po + (k2 >> 1) * MS);
+      else if (k2 == 16) v[k2] = buf_ld2s(rs, mid, po);
+      else {
+        const int q = 31 - k2;
+        v[k2] = buf_ld2s(rs, (q & 1) ? hi1 : hi0, po + (q >> 1) * MS);
+      }
+    }
+  };
   float acc[kL];
 #pragma unroll
   for (int k = 0; k < kL; ++k) acc[k] = 0.0f;
-
+  const PaddedScratch<kR> sc{scratch + grp * kR * (kR + 1)};
+  float2 v[32];
+  load_plane(v, 0);
+  __syncthreads();  // tw visible
 #pragma unroll 1
   for (int p = 0; p < P; ++p) {
-    lds_barrier();  // previous plane's scratch use is over (also publishes tw)
-    {
-      const float2* cb = jbase + (size_t)p * kPlaneB;
-      float4 late[PER - PF > 0 ? PER - PF : 1];
-#pragma unroll
-      for (int i = PF; i < PER; ++i) {
-        const int c = threadIdx.x + 256 * i;
-        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-        late[i - PF] = ld_stream4(cb + (size_t)line * kN + y0 + r2);
-      }
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int c = threadIdx.x + 256 * i;
-        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-        const float4 q = i < PF ? pre[i] : late[i - PF];
-        tile[tile_pos<kR, kGPB>(line, r2)] = make_float2(q.x, q.y);
-        tile[tile_pos<kR, kGPB>(line, r2 + 1)] = make_float2(q.z, q.w);
-      }
-    }
-    if (p + 1 < P) {  // next plane's tile in flight under this plane's FFT
-      const float2* nb = jbase + (size_t)(p + 1) * kPlaneB;
-#pragma unroll
-      for (int i = 0; i < PF; ++i) {
-        const int c = threadIdx.x + 256 * i;
-        const int line = c / (kGPB / 2), r2 = (c % (kGPB / 2)) * 2;
-        pre[i] = ld_stream4(nb + (size_t)line * kN + y0 + r2);
-      }
-    }
-    lds_barrier();
-    float2 v[32];   // slot layout: lane k1, register k2 -> kx = k1 + 28 k2
-#pragma unroll
-    for (int k2 = 0; k2 < 32; ++k2) v[k2] = tile[tile_pos<kR, kGPB>(k1 + kL * k2, grp)];
-    lds_barrier();  // tile consumed: reuse it as transpose scratch
-    fft896_sn<true, kInvScalar>(v, t, PaddedScratch<kR>{tile + grp * kR * (kR + 1)}, tw);
+    fft896_sn<true, kInvScalar>(v, t, sc, tw);      // slot layout in, natural out: x = t + 32 j
 #pragma unroll
     for (int k = 0; k < kL; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
     if (field_out) {  // exact field of this plane (incremental mode init / refresh)
@@ -404,6 +400,7 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
 #pragma unroll
       for (int k = 0; k < kL; ++k) frow[t + kR * k] = v[k];
     }
+    load_plane(v, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
   }
 
   const float invp = 1.0f / (float)P;

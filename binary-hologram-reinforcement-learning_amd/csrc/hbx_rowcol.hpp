@@ -91,4 +91,68 @@ __device__ __forceinline__ int xcd_pair(int bid) {
   else return bid;
 }
 
+// ---------------------------------------------------------------------------
+// Staged slot-tile stores of the column passes (k_col2 at N = 1024 / 256, k_col896 since r04):
+// the output line sets of a block (TL lines: group g = slot g of slot tile st, TileB) go out
+// through the groups' FFT scratch regions.  The writer puts row y of its line at col2_pos(g / 2,
+// y) of its OWN region (no block barrier); after a block barrier col2_stage_store stores the set
+// as 16-B chunks (slots 2 sp, 2 sp + 1 from regions 2 sp, 2 sp + 1) in memory order -- one
+// contiguous run per 16-row band.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int R>
+constexpr int col2_region_stride() { return R * (R + 1) > R * R + 32 ? R * (R + 1) : R * R + 32; }
+template <int R>
+__device__ __forceinline__ float2* col2_region(float2* scratch, int g) {
+  return scratch + g * col2_region_stride<R>();
+}
+// Where row y of slot pair sp's regions sits.  The readers (col2_stage_store) load the rows
+// y0 = band * 16 + (tid / NSP) % 16 of the NSP = TL / 2 slot pairs sp = tid % NSP; gfx950 serves
+// the compiler's ds_read2(st64)_b64 as 16-lane groups over 32 banks (16 float2: NSP pairs x
+// 16 / NSP rows) and a ds_read_b64 as 32-lane groups over 64 banks (NSP pairs x 32 / NSP rows).
+// A constant shift per pair cannot serve both (r03's (sp * 64 / TL) was the 64-bank one; the
+// compiler emits read2st64, and rocprofv3 counted 67.1 M SQ_LDS_BANK_CONFLICT cycles per 128-job
+// k_col2 launch = 8 extra cycles on each of the 32 stage reads per wave and line).  Shift sp by
+// 32 / TL float2 and flip row bit 4 (+16 banks) when row bit HB (the bit splitting a 32-lane
+// group's rows in halves) is set, except for the last pair: conflict-free in both models, and
+// the writers' 16-lane runs of consecutive rows stay conflict-free (tools/lds_swizzle_model.py
+// checks all three; found by exhaustive search over this family).
+template <int R>
+__device__ __forceinline__ int col2_pos(int sp, int y) {
+  constexpr int TL = 256 / R, NSP = TL / 2, HB = ilog2c(16 / NSP);
+  return sp * (32 / TL) + (y ^ ((((y >> HB) & 1) && sp != NSP - 1) ? 16 : 0));
+}
+
+template <int R, int N = R * R>
+__device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu_buffer_rsrc_t rb, int st) {
+  constexpr int TL = 256 / R, CH = N * TL / 2;   // 16-B chunks per line set (N = 896: R = 32's geometry)
+  static_assert(CH % 256 == 0, "whole chunk rounds");
+  // chunk c = tid + 256 i: band c / (8 TL) = tid / (8 TL) + (32 / TL) i, row (tid / (TL / 2)) % 16,
+  // slot pair tid % (TL / 2); memory offset = lane part + i (32 / TL) 16 N + st 16 TL (soffset)
+  const int tid = threadIdx.x, sp = tid % (TL / 2);
+  const int band0 = tid / (8 * TL), r = (tid / (TL / 2)) % 16;
+  const int y0 = band0 * 16 + r;
+  // rows y0 + (32 / TL) 16 i differ from y0 in bits >= 5 only, so col2_pos moves with them
+  static_assert((32 / TL) * 16 >= 32, "stage rows step past the swizzled bits");
+  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + col2_pos<R>(sp, y0);
+  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + col2_pos<R>(sp, y0);
+  const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
+#pragma unroll
+  for (int i = 0; i < CH / 256; ++i) {
+    const float2 lo = lo_r[(32 / TL) * 16 * i];   // (rounded by col2_stage_write under SK)
+    const float2 hi = hi_r[(32 / TL) * 16 * i];
+    const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
+    // non-temporal (nt): B streams out without taking Infinity-Cache residency, so its write-back
+    // no longer lands on top of k_rowinv's reads (r03: N = 256 k_col2 0.143 -> 0.128 ms and
+    // k_rowinv 0.140 -> 0.126; N = 1024 2.70 -> 2.66 and 1.474 -> 1.419).
+    // soffset stays the literal 0, the whole offset rides in voffset: LLVM's gfx950 hazard
+    // recognizer inserts the 2 wait states a VALU write of a >64-bit store's data VGPRs needs
+    // only when the MUBUF soffset is not a register -- with an SGPR soffset (r03) it assumed no
+    // hazard and scheduled such writes right behind the store, the cause of the r03 bf16
+    // non-determinism and of the ITER = 1 wrong B rows (tools/hazard_scan.py
+    // now rejects any wide buffer store with a register soffset)
+    __builtin_amdgcn_raw_buffer_store_b128(o, rb, voff + (st * 16 * TL + i * (32 / TL) * 16 * N) * 8, 0, kBufNT);
+  }
+}
+
 }  // namespace hbx
