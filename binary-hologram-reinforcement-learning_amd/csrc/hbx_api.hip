@@ -855,6 +855,43 @@ int hbx_commit_flip_planes(hbx_plan_t p, uint64_t* base_mask, double* base_chan_
   return HBX_OK;
 }
 
+int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, double* base_chan_stats,
+                        float* plane_inten, int32_t* plane_slot, int32_t n_spare_pairs, const int64_t* order,
+                        int64_t n_order, hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                        int64_t accept_cap, int32_t K, int32_t batches, void* stream) {
+  int rc = check_plan(p);
+  if (rc) return rc;
+  if (!base_mask || !target || !base_chan_stats || !plane_inten || !plane_slot || !order || !walk)
+    return fail(HBX_ERR_INVALID, "null buffer");
+  if (accept_cap < 0 || (accept_cap > 0 && (!accept_pos || !accept_psnr)))
+    return fail(HBX_ERR_INVALID, "accept log");
+  if (p->pd.R != 32 && p->pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (K < 1 || K > 256 || K > p->max_jobs || K > n_spare_pairs)
+    return fail(HBX_ERR_INVALID, "K must be in [1, min(256, max_jobs, n_spare_pairs)]");
+  if (batches < 0 || n_order < 0) return fail(HBX_ERR_INVALID, "batches / n_order");
+  HBX_HIP(hipSetDevice(p->device));
+  hipStream_t st = (hipStream_t)stream;
+  const PlanDev& pd = p->pd;
+  PlanDev pdx = pd;
+  pdx.plane_mode = hbx::kPlanesStep;
+  pdx.plane_pool = plane_inten;
+  pdx.plane_slot = plane_slot;
+  pdx.plane_spares = n_spare_pairs;
+  pdx.spare_base = 0;
+  auto step = [&](int decide) {
+    return hbx::launch_walk_planes(walk, order, p->jobs, pd.job_stats, K, decide, base_mask, base_chan_stats,
+                                   plane_slot, accept_pos, accept_psnr, accept_cap, pd.G, pd.P, pd.N, pd.N,
+                                   pixel_count(p), p->optics.rel_scale, p->optics.peak, st);
+  };
+  HBX_HIP(step(0));                        // this call's first batch of jobs, from the walk state
+  for (int b = 0; b < batches; ++b) {
+    HBX_HIP(hbx::run_jobs(pdx, p->jobs, K, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,
+                          nullptr, st));
+    HBX_HIP(step(1));
+  }
+  return HBX_OK;
+}
+
 int hbx_eval_flips_psf(hbx_plan_t p, const uint64_t* base_mask, const float* target,
                        const double* base_chan_stats, const float* field, const float* intensity,
                        const int64_t* flips, int32_t K, double* psnr_out, double* group_stats,

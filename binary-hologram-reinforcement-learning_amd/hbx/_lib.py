@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "hbx_env_step_psf", "hbx_field_refresh", "hbx_simulate", "hbx_flip_map",
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
     "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
-    "hbx_planes_fill", "hbx_eval_flips_planes", "hbx_commit_flip_planes",
+    "hbx_planes_fill", "hbx_eval_flips_planes", "hbx_commit_flip_planes", "hbx_dbs_walk_planes",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -130,6 +130,7 @@ def _declare(lib):
     lib.hbx_planes_fill.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP]
     lib.hbx_eval_flips_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I32, VP, VP, VP]
     lib.hbx_commit_flip_planes.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP, VP, I32, VP]
+    lib.hbx_dbs_walk_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I64, VP, VP, VP, I64, I32, I32, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_set_timing_sampled.argtypes = [VP, I32, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),

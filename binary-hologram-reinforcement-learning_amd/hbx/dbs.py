@@ -358,6 +358,82 @@ class _Walk:
                             bool(st.stopped_early), acc_t, last, self.seconds)
 
 
+def walk_k_planes(q: float, k_min: int = 1, k_max: int = 64, t0: float = 60.0, c: float = 16.0,
+                  fill: int = 8) -> int:
+    """Speculation depth of the FFT-mode plane-cached walk for acceptance rate q: K minimising
+    the batch time / expected candidates visited, with the batch time t0 (us, the latency of a
+    few-job launch sequence) until K exceeds `fill` candidates and c us per candidate beyond
+    (1024 x 24: a 128-job plane-cached step is 2.08 ms = 16 us per candidate)."""
+    q = min(max(q, 1e-6), 1.0)
+    best, bk = math.inf, k_min
+    for k in range(max(1, k_min), max(k_min, k_max) + 1):
+        vis = (1.0 - (1.0 - q) ** k) / q
+        cost = (t0 + c * max(0, k - fill)) / vis
+        if cost < best:
+            best, bk = cost, k
+    return bk
+
+
+class _PlanesWalk(_Walk):
+    """Host side of the device-decided FFT-mode walk (hbx_dbs_walk_planes): the same two
+    chunks in flight as _Walk, no refreshes (the FFT mode is exact), K from walk_k_planes."""
+
+    def _setup(self, plan, mask, target, total, stop_diff, k_min, k_max, refresh_every, dev, s):
+        self.k_hi = max(1, min(k_max, plan.max_jobs, 256))
+        self.pool = plan.plane_pool(self.k_hi)
+        stats, psnr0 = plan.planes_fill(mask, target, *self.pool, stream=s)
+        self.base_stats = stats.contiguous()
+        self.init = float(psnr0.item())
+        w = _lib.DbsWalk()
+        w.total = total
+        w.prev_psnr = w.init_psnr = self.init
+        w.last_psnr = math.nan
+        w.stop_enabled = 1 if stop_diff is not None else 0
+        w.stop_diff = float(stop_diff) if stop_diff is not None else 0.0
+        w.commit_ch = -1
+        self.st = w
+        nbytes = C.sizeof(_lib.DbsWalk)
+        self.wbuf = torch.frombuffer(bytearray(bytes(w)), dtype=torch.uint8).to(dev)
+        self.cap = max(1, total)
+        self.log_pos = torch.empty(self.cap, dtype=torch.int64, device=dev)
+        self.log_psnr = torch.empty(self.cap, dtype=torch.float64, device=dev)
+        self.pinned = [torch.empty(nbytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.events = [torch.cuda.Event(), torch.cuda.Event()]
+        self.k_lo = max(1, k_min)
+        self.q, self.pos_prev, self.acc_prev = 0.5, 0, 0
+        self.fused = False
+        self.k = walk_k_planes(self.q, self.k_lo, self.k_hi)
+        self.marks, self.exact = [], {}
+        self.issued = self.done_n = 0
+        self.finished = False
+        self.t0 = time.perf_counter()
+
+    def _chunk_n(self, stream, batches):
+        self.plan.dbs_walk_planes(self.mask, self.target, self.base_stats, *self.pool, self.order_t, self.wbuf,
+                                  self.log_pos, self.log_psnr, self.k, batches, stream=stream)
+
+    def advance(self):
+        if self.finished:
+            return
+        st = self.st = self.take()
+        self.marks.append((int(st.accepted), time.perf_counter() - self.t0))
+        if self.progress is not None:
+            self.progress(int(st.pos), int(st.accepted), float(st.prev_psnr), self.marks[-1][1])
+        dpos, dacc = st.pos - self.pos_prev, st.accepted - self.acc_prev
+        if dpos > 0:
+            self.q = 0.5 * self.q + 0.5 * (dacc / dpos)
+            self.k = walk_k_planes(self.q, self.k_lo, self.k_hi)
+        self.pos_prev, self.acc_prev = st.pos, st.accepted
+        if st.done:
+            while self.done_n < self.issued:
+                self.take()
+            self.s.synchronize()
+            self.finished = True
+            self.seconds = time.perf_counter() - self.t0
+            return
+        self.issue()
+
+
 def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_max, stream,
                  refresh_every, chunk: int = 64, progress=None, graphs: bool = False) -> GreedyResult:
     """greedy(mode="psf") on the device-resident walk (hbx_dbs_walk_psf)."""
@@ -425,7 +501,7 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
            stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None,
-           graphs: bool = False, planes: Optional[bool] = None) -> GreedyResult:
+           graphs: bool = False, planes: Optional[bool] = None, device_walk: Optional[bool] = None) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
     mode="fft": every candidate is the FFT-mode propagation of its colour group
@@ -433,7 +509,9 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     state's per-plane |U_p|^2 (hbx_eval_flips_planes, ABI v10): a candidate propagates
     only its flipped plane's pair and sums the cached planes in the same order, so its
     PSNR -- and the accept sequence -- is the full re-propagation's bit for bit;
-    planes=False re-propagates all P planes of the group per candidate.
+    planes=False re-propagates all P planes of the group per candidate.  device_walk (default:
+    on with planes) decides each batch on the device (hbx_dbs_walk_planes: no host round trip
+    per batch, the host reads the walk state every 64 batches); False decides on the host.
     mode="psf": candidates are evaluated on the incremental-field path, the
     whole walk device-resident (hbx_dbs_walk_psf); the base fields are
     re-propagated exactly every ``refresh_every`` accepted flips.
@@ -457,6 +535,15 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
         planes = mode == "fft" and plan.cfg.height in (256, 1024)
     if planes and (mode != "fft" or plan.cfg.height not in (256, 1024)):
         raise ValueError("planes=True is the FFT mode's plane cache at N = 1024 / 256")
+    if device_walk is None:
+        device_walk = planes
+    if device_walk:
+        if not planes:
+            raise ValueError("device_walk=True runs on the plane cache (planes=True)")
+        w = _PlanesWalk(plan, mask, target, order_t, total, stop_diff, 1, k_max, stream, 0, progress=progress)
+        while not w.finished:
+            w.advance()
+        return w.result()
     pool = None
     if planes:
         pool = plan.plane_pool(k_max)

@@ -353,6 +353,27 @@ class Plan:
                                                    _ptr(group_stats), _ptr(k_dev), k, _stream(stream)),
                    "hbx_commit_flip_planes")
 
+    def dbs_walk_planes(self, base_mask, target, base_stats, plane_inten, plane_slot, order: torch.Tensor,
+                        walk: torch.Tensor, accept_pos: torch.Tensor, accept_psnr: torch.Tensor, K: int,
+                        batches: int, stream=None):
+        """hbx_dbs_walk_planes: enqueue `batches` device-decided batches of K candidates of the
+        FFT-mode greedy on the base state's plane pool (no host round trip)."""
+        c = self.cfg
+        _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
+        _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
+        _need(base_stats, "base_stats", torch.float64, (c.groups, 3), self.device)
+        s = self._check_pool(plane_inten, plane_slot)
+        _need(order, "order", torch.int64, (order.shape[0],), self.device)
+        _need(walk, "walk", torch.uint8, (C.sizeof(_lib.DbsWalk),), self.device)
+        cap = accept_pos.shape[0]
+        _need(accept_pos, "accept_pos", torch.int64, (cap,), self.device)
+        _need(accept_psnr, "accept_psnr", torch.float64, (cap,), self.device)
+        _lib.check(self.lib.hbx_dbs_walk_planes(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                                _ptr(plane_inten), _ptr(plane_slot), s, _ptr(order),
+                                                int(order.shape[0]), _ptr(walk), _ptr(accept_pos),
+                                                _ptr(accept_psnr), cap, int(K), int(batches), _stream(stream)),
+                   "hbx_dbs_walk_planes")
+
     def eval_flips_psf(self, base_mask, target, base_stats, field, intensity, flips,
                        psnr_out=None, group_stats=None, stream=None):
         """eval_flips on the incremental-field path: field [CH, H, W, 2] f32 and

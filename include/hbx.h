@@ -281,6 +281,7 @@ int hbx_commit_flip_planes(hbx_plan_t plan, uint64_t* base_mask, double* base_ch
                            const int64_t* flips, const double* psnr_out, const double* group_stats,
                            const int32_t* k, int32_t K, void* stream);
 
+
 /* hbx_eval_flips / hbx_commit_flip on the incremental-field path: the base
  * env additionally carries its per-plane field [CH][H][W][2] and group
  * intensities [G][H][W] (hbx_simulate), so a candidate costs one streaming
@@ -371,6 +372,23 @@ int hbx_dbs_walk_psf(hbx_plan_t plan, uint64_t* base_mask, const float* target,
                      double* base_chan_stats, float* field, float* intensity, const int64_t* order,
                      int64_t n_order, hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
                      int64_t accept_cap, int32_t K, int32_t batches, void* stream);
+
+/* (ABI v10) The same greedy DBS with the decision on the device: `batches`
+ * speculative batches of K candidates (order[pos .. pos + K)) are enqueued
+ * without a host round trip; after each batch's propagation one block forms
+ * the K PSNRs (as hbx_eval_flips_planes), commits the first strict improvement
+ * (as hbx_commit_flip_planes) into base_mask / base_chan_stats / plane_slot,
+ * logs it (accept_pos / accept_psnr, up to accept_cap) and advances the walk
+ * state (hbx_dbs_walk_t: pos, total, accepted, batches, prev / init / last
+ * PSNR, stop_enabled / stop_diff, done, stopped_early; the incremental-walk
+ * fields are unused).  Batches after `done` are no-ops.  K <= n_spare_pairs,
+ * max_jobs and 256.  The accept sequence and every logged PSNR are the
+ * host-decided batches' (and the full re-propagation's) bit for bit. */
+int hbx_dbs_walk_planes(hbx_plan_t plan, uint64_t* base_mask, const float* target,
+                        double* base_chan_stats, float* plane_inten, int32_t* plane_slot,
+                        int32_t n_spare_pairs, const int64_t* order, int64_t n_order,
+                        hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                        int64_t accept_cap, int32_t K, int32_t batches, void* stream);
 
 /* Incremental-field ("PSF") mode (reported separately from
  * the FFT-mode headline).  tt.simulate is linear, so flipping pixel (c, r, col)

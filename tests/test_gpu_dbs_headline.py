@@ -196,20 +196,23 @@ def test_fft_greedy_plane_cache_equals_full_repropagation(golden_dir, name, stop
     d, ocfg, pre, tgt, order = _fixture(golden_dir, name)
     n = int(d["n"])
     runs = {}
-    for planes in (False, True):
+    for planes, walk in ((False, False), (True, False), (True, True)):
         plan, mask, target = _dev(ocfg, pre, tgt)
-        res = dbs.greedy(plan, mask, target, order[:n], stop_diff=stop, mode="fft", planes=planes)
-        runs[planes] = (res, mask.cpu().numpy())
+        res = dbs.greedy(plan, mask, target, order[:n], stop_diff=stop, mode="fft", planes=planes,
+                         device_walk=walk)
+        runs[(planes, walk)] = (res, mask.cpu().numpy())
         plan.close()
-    (full, m_full), (cached, m_cached) = runs[False], runs[True]
-    print(f"{name}: {cached.steps} candidates, {len(cached.accepted_positions)} accepts, "
-          f"{cached.launches} batches")
-    assert cached.accepted_positions == full.accepted_positions
-    assert cached.accepted_psnr == full.accepted_psnr                 # bit for bit
-    assert cached.initial_psnr == full.initial_psnr and cached.final_psnr == full.final_psnr
-    assert cached.steps == full.steps and cached.stopped_early == full.stopped_early
-    assert np.array_equal(m_full, m_cached)
-    assert len(cached.accepted_positions) > 100
+    full, m_full = runs[(False, False)]
+    for key in ((True, False), (True, True)):    # host-decided and device-decided batches
+        cached, m_cached = runs[key]
+        print(f"{name} planes / device walk {key}: {cached.steps} candidates, "
+              f"{len(cached.accepted_positions)} accepts, {cached.launches} batches")
+        assert cached.accepted_positions == full.accepted_positions, key
+        assert cached.accepted_psnr == full.accepted_psnr, key            # bit for bit
+        assert cached.initial_psnr == full.initial_psnr and cached.final_psnr == full.final_psnr, key
+        assert cached.steps == full.steps and cached.stopped_early == full.stopped_early, key
+        assert np.array_equal(m_full, m_cached), key
+    assert len(full.accepted_positions) > 100
 
 
 def test_candidate_change_precision_1024x24(golden_dir):
