@@ -648,7 +648,12 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
       pdx.plane_pool = e->plane_inten + (size_t)b0 * (CH + 2) * hw;
       pdx.plane_slot = e->plane_slot + (size_t)b0 * (CH + 2);
     }
-    if (to_recon)   // the previous step's group: recon and intensity agree again before it is overwritten
+    // the previous step's group: recon and intensity agree again before it is overwritten -- in
+    // k_rowinv_d's epilogue at N = 1024 / 256 (no launch of its own), else k_recon_reconcile
+    const bool fuse_rc = to_recon && (pd.R == 32 || pd.R == 16);
+    pdx.rc_pending = fuse_rc ? ed.recon_pending : nullptr;
+    pdx.rc_cache = fuse_rc ? e->intensity + (size_t)b0 * G * hw : nullptr;
+    if (to_recon && !fuse_rc)
       HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
     HBX_HIP(hbx::run_jobs(pdx, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,

@@ -145,6 +145,10 @@ struct PlanDev {
   int plane_spares;          // S: spare pairs per env (0 / 1: the env step's one pair).  S > 1 (ABI v10,
                              // hbx_eval_flips_planes): candidate j of a launch writes its pair to spare
   int spare_base;            // pair spare_base + j, so K candidates of one base keep K fresh pairs
+  // (r04) env step with the recon observation at N = 1024 / 256: k_rowinv_d applies the previous
+  // step's recon / intensity-cache reconcile (recon_pending, env-major like inten_out) itself
+  const int32_t* rc_pending; // [env] nullable
+  float* rc_cache;           // [env][G][N][N] the intensity cache
 };
 constexpr int kPlanesOff = 0, kPlanesFill = 1, kPlanesStep = 2;
 

@@ -164,7 +164,9 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     if (term_out) term_out[b] = 0;
     if (trunc_out) trunc_out[b] = 0;
     if (accept_flag) accept_flag[b] = 0;
-    if (env.recon_pending) env.recon_pending[b] = 0;
+    // recon_pending stays: an invalid job propagates nothing, so the previous step's reconcile
+    // (fused into k_rowinv_d, which skips invalid jobs) is still owed and the next valid step
+    // applies it (the separate k_recon_reconcile of the other sizes is idempotent)
     return;
   }
   const int g = jb.group;

@@ -551,7 +551,9 @@ template <int R, int GPB>
 __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, const JobDesc& jb, int j, int y,
                                                 int rb, int grp, int t, const float* __restrict__ target,
                                                 size_t tmask, float* __restrict__ inten_out, int inten_by_env,
-                                                double* __restrict__ partial, double (&red)[GPB][3]) {
+                                                double* __restrict__ partial, double (&red)[GPB][3],
+                                                const int32_t* __restrict__ rc_pending = nullptr,
+                                                float* __restrict__ rc_cache = nullptr) {
   constexpr int N = R * R;
   constexpr int RB = N / GPB;
   const float invp = 1.0f / (float)P;
@@ -571,6 +573,26 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
   if (inten_out) {
     const size_t slot = inten_by_env ? (size_t)jb.env * G + jb.group : (size_t)j;
     float* orow = inten_out + (slot * N + y) * N;
+    if (rc_pending) {
+      // (r04) the previous step's recon / intensity-cache reconcile of this env, fused here
+      // instead of its own launch before the step (k_recon_reconcile): the previous step left
+      // group gp's new intensity in recon only (p > 0, accepted: recon -> cache) or its stepped
+      // intensity in recon (p < 0, rolled back: cache -> recon).  Row y of group gp is moved
+      // by the lane group of row y; when gp is this step's group, an accepted row is read out
+      // before this step overwrites it and a rolled-back one needs nothing.
+      const int p = rc_pending[jb.env];
+      if (p != 0) {
+        const int gp = (p > 0 ? p : -p) - 1;
+        const size_t grow = (((size_t)jb.env * G + gp) * N + y) * N;
+        if (p > 0) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) rc_cache[grow + t + R * k] = inten_out[grow + t + R * k];
+        } else if (gp != jb.group) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) inten_out[grow + t + R * k] = rc_cache[grow + t + R * k];
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
   }
@@ -609,7 +631,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
                                                      float2* __restrict__ field_out, size_t tmask, int inten_by_env,
                                                      int plane_mode, float* __restrict__ plane_pool,
                                                      const int32_t* __restrict__ plane_slot, int plane_spares,
-                                                     int spare_base) {
+                                                     int spare_base, const int32_t* __restrict__ rc_pending,
+                                                     float* __restrict__ rc_cache) {
   constexpr int N = R * R, GPB = 256 / R, RB = N / GPB, TL = 256 / R;
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
@@ -706,7 +729,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
     finish_plane(va, pa + 1);
 #pragma unroll 1
     for (int q = pa + 2; q < P; ++q) add_cached(q);
-    rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
+    rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red,
+                           rc_pending, rc_cache);
     return;
   }
   load_plane(va, 0);
@@ -727,7 +751,8 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
       load_plane(va, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
     }
   }
-  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red);
+  rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red,
+                           rc_pending, rc_cache);
 }
 
 template <int R, int NT>
@@ -1018,7 +1043,7 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
       hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
                          pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
                          pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot, pd.plane_spares,
-                         pd.spare_base);
+                         pd.spare_base, pd.rc_pending, pd.rc_cache);
     else
       hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                          target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
