@@ -363,17 +363,16 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
 // Scalar-f32 FFTs: with two lines in registers the packed variant spills.
 // Measured and removed: the round-1 LDS mirror, packed DFTs,
 // three workgroups per CU, H issued ahead, B panels of 8 / 32 / 64 rows.
-template <int R>
+//
 // Lines per lane group.  Measured r03: N = 1024 ITER 2 / 4 / 8 = 2.94 / 2.72 / 2.76 ms (with the
-// nt B stores, r03i: 2.82 / 2.58-2.60 / 2.68-2.70).  N = 256:
-// ITER 4 = 0.152 ms, 2 = 0.144; ITER 1 timed 0.142 but wrote wrong B rows (193-223, odd, in
-// workgroups >= 256 only; not an uninitialised-LDS read: NaN-filled scratch changes nothing)
-// -- not understood, so not used (profiles/r03/kcol2_iter1_anomaly.txt).
-#ifdef HBX_COL2_ITER1   // r04 re-check of the ITER = 1 anomaly with soffset-0 stage stores (exp build only)
-__host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : 1; }
-#else
+// nt B stores, r03i: 2.82 / 2.58-2.60 / 2.68-2.70).  N = 256: ITER 4 = 0.152 ms, 2 = 0.144.  r03's
+// ITER = 1 build wrote wrong B rows; the cause was the wide-store data hazard of the SGPR-soffset
+// stage stores.  Rebuilt with the soffset-0 stores (r04) it is exact (the 256 flip
+// map / mono / plane tests, profiles/r04/iter1_tests_r04b.txt) and no faster (0.1445-0.1447 ms vs
+// 0.1432-0.1445 for ITER = 2, profiles/r04/iter1_ab_r04b.txt), so ITER = 2 stays; small launches
+// use ITER = 1 (launch_passes' kSmallBlocks).
+template <int R>
 __host__ __device__ constexpr int col2_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }
-#endif
 
 // N = 1024 / 256: the output line sets of a k_col2 block (TL lines: group g = slot g of
 // slot tile st, TileB) go out through the FFT scratch.  col2_stage_write: each group
