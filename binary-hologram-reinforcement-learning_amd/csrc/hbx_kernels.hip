@@ -369,96 +369,101 @@ __global__ void k_commit_flip(uint64_t* __restrict__ mask, double* __restrict__ 
 }
 
 // Device-decided greedy DBS in the FFT mode with the base state's plane cache (ABI v10,
-// hbx_dbs_walk_planes): one block.  decide = 1: the K candidates of the batch just propagated
-// (jobs[k] = order[pos + k]) get their PSNR exactly as k_eval_finalize forms it; the first that
-// strictly improves (DBS_1024_24.py:355) is committed as hbx_commit_flip_planes does (mask bit,
-// group stats, prev PSNR, the pair's spare slots swapped in) and logged; the walk advances past
-// it (or past the whole batch).  Then -- decide = 0 too -- the NEXT batch's K jobs are written
-// from the walk state (invalid jobs once the walk is done, so the passes behind return at once).
+// hbx_dbs_walk_planes): one block.  decide = 1: the candidates of the batch just propagated
+// (jobs[c] = order[pos + c], each propagated against the batch's base state) are visited in order
+// by one thread, exactly as the serial loop (DBS_1024_24.py:313-363) visits them: a candidate's
+// PSNR is formed from its group's propagated stats and the CURRENT stats of the other groups
+// (k_eval_finalize's sum order), and the first strict improvement (:355) is committed as
+// hbx_commit_flip_planes does (mask bit, group stats, prev PSNR, the pair's spare slots swapped
+// in) and logged.  The visit then CONTINUES: a later candidate of a colour group no accept of
+// this batch has touched was propagated against exactly the group state the serial loop would
+// propagate it against (the other groups enter only through their stats), so its PSNR is the
+// serial loop's bit for bit; the batch ends before the first candidate of a touched group (it
+// needs a fresh propagation) -- up to G accepts per batch.  Then -- decide = 0 too -- the NEXT
+// batch's K jobs are written from the walk state (invalid jobs once the walk is done, so the
+// passes behind return at once).
+__device__ __forceinline__ double js_get(const double* js, int c, int i) { return js[3 * (size_t)c + i]; }
+
 __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __restrict__ order,
                               JobDesc* __restrict__ jobs, const double* __restrict__ job_stats, int K, int decide,
                               uint64_t* __restrict__ mask, double* __restrict__ base_stats,
                               int32_t* __restrict__ plane_slot, int64_t* __restrict__ accept_pos,
                               double* __restrict__ accept_psnr, int64_t accept_cap, int G, int P, int H, int W,
                               double count, int rel_scale, double peak) {
-  __shared__ int s_first;
   __shared__ int64_t s_pos;
   __shared__ int s_done;
   const int k = threadIdx.x;
   const int64_t hw = (int64_t)H * W;
   if (k == 0) {
-    s_first = K;
     s_pos = w->pos;
     s_done = w->done;
-  }
-  __syncthreads();
-  if (decide && !s_done) {
-    const int64_t pos = s_pos;
-    const int nk = (int)min((int64_t)K, w->total - pos);
-    const double prev = w->prev_psnr;
-    double ps = 0.0;
-    if (k < nk) {
-      const JobDesc jb = jobs[k];
-      const double* js = job_stats + 3 * (size_t)k;
-      double sxy = 0.0, sxx = 0.0, syy = 0.0;
-      for (int gg = 0; gg < G; ++gg) {    // k_eval_finalize's sum order
-        if (gg == jb.group) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
-        else { sxy += base_stats[3 * gg]; sxx += base_stats[3 * gg + 1]; syy += base_stats[3 * gg + 2]; }
+    if (decide && !s_done) {
+      const int64_t pos = s_pos;
+      const int nk = (int)min((int64_t)K, w->total - pos);
+      double prev = w->prev_psnr, last = w->last_psnr;
+      int64_t a = w->accepted;
+      unsigned touched = 0;
+      int visited = nk, done = 0;
+      for (int c = 0; c < nk; ++c) {
+        const JobDesc jb = jobs[c];
+        if (jb.env >= 0 && ((touched >> jb.group) & 1u)) { visited = c; break; }
+        double ps = NAN;
+        if (jb.env >= 0) {
+          const double* js = job_stats + 3 * (size_t)c;
+          double sxy = 0.0, sxx = 0.0, syy = 0.0;
+          for (int gg = 0; gg < G; ++gg) {    // k_eval_finalize's sum order
+            if (gg == jb.group) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
+            else { sxy += base_stats[3 * gg]; sxx += base_stats[3 * gg + 1]; syy += base_stats[3 * gg + 2]; }
+          }
+          ps = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
+        }
+        last = ps;
+        if (ps > prev) {                     // commit candidate c
+          const int ch = jb.group * P + jb.flip_plane;
+          const int pix = jb.flip_pix;
+          mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64] ^=
+              (1ull << ((pix % W) & 63));
+          base_stats[3 * jb.group] = js_get(job_stats, c, 0);
+          base_stats[3 * jb.group + 1] = js_get(job_stats, c, 1);
+          base_stats[3 * jb.group + 2] = js_get(job_stats, c, 2);
+          const int CH = G * P, pa = jb.group * P + (jb.flip_plane & ~1);
+          for (int q = 0; q < 2; ++q) {
+            const int32_t cur = plane_slot[pa + q];
+            plane_slot[pa + q] = plane_slot[CH + 2 * c + q];
+            plane_slot[CH + 2 * c + q] = cur;
+          }
+          if (a < accept_cap) { accept_pos[a] = pos + c; accept_psnr[a] = ps; }
+          ++a;
+          prev = ps;
+          touched |= 1u << jb.group;
+          if (w->stop_enabled && ps - w->init_psnr >= w->stop_diff) {   // DBS_ratio_0.5.py:366-372
+            done = 1;
+            w->stopped_early = 1;
+            visited = c + 1;
+            break;
+          }
+        }
       }
-      ps = jb.env < 0 ? NAN : psnr_from(sxy, sxx, syy, count, rel_scale, peak);
-      if (ps > prev) atomicMin(&s_first, k);
-    }
-    __syncthreads();
-    const int i = s_first;
-    if (i < nk && k == i) {               // commit candidate i
-      const JobDesc jb = jobs[i];
-      const int ch = jb.group * P + jb.flip_plane;
-      const int pix = jb.flip_pix;
-      mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64] ^= (1ull << ((pix % W) & 63));
-      const double* js = job_stats + 3 * (size_t)i;
-      base_stats[3 * jb.group] = js[0];
-      base_stats[3 * jb.group + 1] = js[1];
-      base_stats[3 * jb.group + 2] = js[2];
-      const int CH = G * P, pa = jb.group * P + (jb.flip_plane & ~1);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int32_t cur = plane_slot[pa + q];
-        plane_slot[pa + q] = plane_slot[CH + 2 * i + q];
-        plane_slot[CH + 2 * i + q] = cur;
-      }
-      const int64_t a = w->accepted;
-      if (a < accept_cap) { accept_pos[a] = pos + i; accept_psnr[a] = ps; }
-      w->accepted = a + 1;
-      w->prev_psnr = ps;
-      w->last_psnr = ps;
-      w->pos = pos + i + 1;
-      if (w->stop_enabled && ps - w->init_psnr >= w->stop_diff) {   // DBS_ratio_0.5.py:366-372
-        w->done = 1;
-        w->stopped_early = 1;
-      }
-    }
-    if (i >= nk && k == nk - 1) {         // no accept: the whole batch is visited
-      w->last_psnr = ps;
-      w->pos = pos + nk;
-    }
-    __syncthreads();
-    if (k == 0) {
+      w->accepted = a;
+      w->prev_psnr = prev;
+      w->last_psnr = last;
+      w->pos = pos + visited;
       w->batches += 1;
-      if (w->pos >= w->total) w->done = 1;
+      if (done || w->pos >= w->total) w->done = 1;
       s_pos = w->pos;
       s_done = w->done;
     }
-    __syncthreads();
   }
+  __syncthreads();
   if (k < K) {                            // the next batch's jobs
     const int64_t q = s_pos + k;
     JobDesc jd;
     jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
     if (!s_done && q < w->total) {
-      const int64_t a = order[q];
-      if (a >= 0 && a < (int64_t)G * P * hw) {
-        const int ch = (int)(a / hw);
-        jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(a % hw);
+      const int64_t av = order[q];
+      if (av >= 0 && av < (int64_t)G * P * hw) {
+        const int ch = (int)(av / hw);
+        jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(av % hw);
       }
     }
     jobs[k] = jd;

@@ -358,17 +358,36 @@ class _Walk:
                             bool(st.stopped_early), acc_t, last, self.seconds)
 
 
-def walk_k_planes(q: float, k_min: int = 1, k_max: int = 64, t0: float = 60.0, c: float = 16.0,
-                  fill: int = 8) -> int:
+def planes_visited(q: float, k: int, groups: int) -> float:
+    """Expected candidates a device-decided FFT-mode batch of k visits (hbx_dbs_walk_planes): the
+    batch runs until the first candidate of a colour group an accept of this batch has touched
+    (each candidate's group uniform over `groups`, accepted with probability q)."""
+    dist = [1.0] + [0.0] * groups              # P(m groups touched, batch still running)
+    vis = 0.0
+    for _ in range(k):
+        nxt = [0.0] * (groups + 1)
+        for m, pm in enumerate(dist):
+            if pm:
+                cont = pm * (1.0 - m / groups)
+                vis += cont
+                nxt[m] += cont * (1.0 - q)
+                if m < groups:
+                    nxt[m + 1] += cont * q
+        dist = nxt
+    return vis
+
+
+def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0: float = 140.0,
+                  c: float = 16.0, fill: int = 8) -> int:
     """Speculation depth of the FFT-mode plane-cached walk for acceptance rate q: K minimising
-    the batch time / expected candidates visited, with the batch time t0 (us, the latency of a
-    few-job launch sequence) until K exceeds `fill` candidates and c us per candidate beyond
-    (1024 x 24: a 128-job plane-cached step is 2.08 ms = 16 us per candidate)."""
+    the batch time / expected candidates visited (planes_visited), with the batch time t0 (us,
+    the latency of a few-job launch sequence, measured ~147 us at 1024 x 24) until K exceeds
+    `fill` candidates and c us per candidate beyond (a 128-job plane-cached step is 2.08 ms =
+    16 us per candidate)."""
     q = min(max(q, 1e-6), 1.0)
     best, bk = math.inf, k_min
     for k in range(max(1, k_min), max(k_min, k_max) + 1):
-        vis = (1.0 - (1.0 - q) ** k) / q
-        cost = (t0 + c * max(0, k - fill)) / vis
+        cost = (t0 + c * max(0, k - fill)) / planes_visited(q, k, groups)
         if cost < best:
             best, bk = cost, k
     return bk
@@ -402,7 +421,7 @@ class _PlanesWalk(_Walk):
         self.k_lo = max(1, k_min)
         self.q, self.pos_prev, self.acc_prev = 0.5, 0, 0
         self.fused = False
-        self.k = walk_k_planes(self.q, self.k_lo, self.k_hi)
+        self.k = walk_k_planes(self.q, plan.cfg.groups, self.k_lo, self.k_hi)
         self.marks, self.exact = [], {}
         self.issued = self.done_n = 0
         self.finished = False
@@ -422,7 +441,7 @@ class _PlanesWalk(_Walk):
         dpos, dacc = st.pos - self.pos_prev, st.accepted - self.acc_prev
         if dpos > 0:
             self.q = 0.5 * self.q + 0.5 * (dacc / dpos)
-            self.k = walk_k_planes(self.q, self.k_lo, self.k_hi)
+            self.k = walk_k_planes(self.q, self.plan.cfg.groups, self.k_lo, self.k_hi)
         self.pos_prev, self.acc_prev = st.pos, st.accepted
         if st.done:
             while self.done_n < self.issued:
