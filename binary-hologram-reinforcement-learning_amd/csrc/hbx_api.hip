@@ -883,8 +883,10 @@ int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, 
   pdx.plane_slot = plane_slot;
   pdx.plane_spares = n_spare_pairs;
   pdx.spare_base = 0;
+  pdx.skip_reduce = 1;                     // k_walk_planes reduces the row-block partials itself
+  const int RB = pd.N / (256 / pd.R);
   auto step = [&](int decide) {
-    return hbx::launch_walk_planes(walk, order, p->jobs, pd.job_stats, K, decide, base_mask, base_chan_stats,
+    return hbx::launch_walk_planes(walk, order, p->jobs, pd.partial, RB, K, decide, base_mask, base_chan_stats,
                                    plane_slot, accept_pos, accept_psnr, accept_cap, pd.G, pd.P, pd.N, pd.N,
                                    pixel_count(p), p->optics.rel_scale, p->optics.peak, st);
   };

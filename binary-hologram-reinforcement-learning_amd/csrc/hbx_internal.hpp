@@ -149,6 +149,7 @@ struct PlanDev {
   // step's recon / intensity-cache reconcile (recon_pending, env-major like inten_out) itself
   const int32_t* rc_pending; // [env] nullable
   float* rc_cache;           // [env][G][N][N] the intensity cache
+  int skip_reduce = 0;       // 1: leave the per-row-block partials (a caller reduces them itself)
 };
 constexpr int kPlanesOff = 0, kPlanesFill = 1, kPlanesStep = 2;
 
@@ -292,8 +293,8 @@ hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, dou
 hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
                                   size_t hw, hipStream_t st);
 // plane cache (ABI v9): slot[env][i] = i for the listed envs (env_ids nullable: 0 .. n_ids - 1)
-hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* job_stats,
-                              int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
+hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* partial,
+                              int RB, int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
                               int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int G, int P, int H,
                               int W, double count, int rel, double peak, hipStream_t st);
 hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CHS, hipStream_t st);

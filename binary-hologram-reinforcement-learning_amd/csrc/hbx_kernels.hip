@@ -385,15 +385,35 @@ __global__ void k_commit_flip(uint64_t* __restrict__ mask, double* __restrict__ 
 __device__ __forceinline__ double js_get(const double* js, int c, int i) { return js[3 * (size_t)c + i]; }
 
 __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __restrict__ order,
-                              JobDesc* __restrict__ jobs, const double* __restrict__ job_stats, int K, int decide,
-                              uint64_t* __restrict__ mask, double* __restrict__ base_stats,
+                              JobDesc* __restrict__ jobs, const double* __restrict__ partial, int RB, int K,
+                              int decide, uint64_t* __restrict__ mask, double* __restrict__ base_stats,
                               int32_t* __restrict__ plane_slot, int64_t* __restrict__ accept_pos,
                               double* __restrict__ accept_psnr, int64_t accept_cap, int G, int P, int H, int W,
                               double count, int rel_scale, double peak) {
   __shared__ int64_t s_pos;
   __shared__ int s_done;
+  constexpr int CJ = 8;                     // jobs per staging round of the partials
+  __shared__ double s_part[CJ * 3 * 128];   // RB <= 128 row blocks
+  __shared__ double s_js[256 * 3];
   const int k = threadIdx.x;
   const int64_t hw = (int64_t)H * W;
+  if (decide) {
+    // k_reduce_partials fused (one launch per batch less): each candidate's three statistics
+    // summed over its row blocks in row-block order, k_reduce_partials' order bit for bit
+    for (int c0 = 0; c0 < K; c0 += CJ) {
+      const int nj = K - c0 < CJ ? K - c0 : CJ;
+      for (int i = k; i < nj * RB * 3; i += blockDim.x) s_part[i] = partial[(size_t)c0 * RB * 3 + i];
+      __syncthreads();
+      if (k < nj * 3) {
+        const int c = k / 3, st = k % 3;
+        double acc = 0.0;
+        for (int i = st; i < 3 * RB; i += 3) acc += s_part[c * 3 * RB + i];
+        s_js[3 * (c0 + c) + st] = acc;
+      }
+      __syncthreads();
+    }
+  }
+  const double* job_stats = s_js;
   if (k == 0) {
     s_pos = w->pos;
     s_done = w->done;
@@ -470,11 +490,12 @@ __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __r
   }
 }
 
-hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* job_stats,
-                              int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
+hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* partial,
+                              int RB, int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
                               int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int G, int P, int H,
                               int W, double count, int rel, double peak, hipStream_t st) {
-  hipLaunchKernelGGL(k_walk_planes, dim3(1), dim3(256), 0, st, w, order, jobs, job_stats, K, decide, mask,
+  if (RB > 128 || K > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_walk_planes, dim3(1), dim3(256), 0, st, w, order, jobs, partial, RB, K, decide, mask,
                      base_stats, plane_slot, accept_pos, accept_psnr, accept_cap, G, P, H, W, count, rel, peak);
   return hipGetLastError();
 }

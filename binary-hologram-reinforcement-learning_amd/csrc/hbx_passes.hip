@@ -1049,8 +1049,9 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
                          field_out, target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
     if (tm) tm->end(2, n_jobs, st);
   }
-  hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial,
-                     n_jobs, N / (kRowNT<R> / R), pd.job_stats);
+  if (!pd.skip_reduce)
+    hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial,
+                       n_jobs, N / (kRowNT<R> / R), pd.job_stats);
   return hipGetLastError();
 }
 

@@ -5,6 +5,8 @@ set -o pipefail
 T=gpurun_out/r04e
 mkdir -p $T
 export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_planes.py tests/test_gpu_dbs_headline.py -m gpu > $T/walk_tests.log 2>&1 || { tail -30 $T/walk_tests.log; exit 19; }
+tail -2 $T/walk_tests.log
 for k in 4 8; do
   timeout -k 10 200 python tools/dbs_walk_bench.py --flips 16384 --trace --k $k >> $T/dbs_walk_k.txt 2>&1 || exit 20
 done
