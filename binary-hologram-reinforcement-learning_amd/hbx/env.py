@@ -151,6 +151,12 @@ class EnvState:
             raise ValueError("action out of range [0, CH*H*W) passed to step()")
 
 
+def _raw_stream(index):
+    """The current HIP stream of device `index` as an integer, without building a
+    torch.cuda.Stream object (torch.cuda.current_stream costs a few us per call)."""
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
 class HologramVecEnv(_VecEnvBase):
     """B environments on one GPU, stepped together -- an SB3 VecEnv (subclass of
     stable_baselines3's VecEnv when it is importable, the same method set otherwise:
@@ -283,7 +289,13 @@ class HologramVecEnv(_VecEnvBase):
         self.state.bufs.error = self.state.error.data_ptr()
         self._host_raw = torch.zeros(self._row_bytes + 8, dtype=torch.uint8,
                                      pin_memory=self.device.type == "cuda")
-        self._host_np = self._host_raw.numpy()
+        self._host_np = h = self._host_raw.numpy()
+        # views of the pinned row, built once: step()'s work between the readback and its return
+        # is on the GPU's critical path (the next step cannot launch before it)
+        self._h_rew = h[:8 * n].view(np.float64)
+        self._h_term, self._h_trunc = h[17 * n:18 * n], h[18 * n:19 * n]
+        self._h_err = h[self._row_bytes:self._row_bytes + 4].view(np.int32)
+        self._dev_index = self.device.index if self.device.type == "cuda" else None
         self._readback = torch.cuda.Event() if self.device.type == "cuda" else None
         self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
@@ -467,7 +479,7 @@ class HologramVecEnv(_VecEnvBase):
         self._last_actions = actions
         a = self._fast_args
         a[4] = actions.data_ptr()
-        a[11] = torch.cuda.current_stream(self.device).cuda_stream
+        a[11] = _raw_stream(self._dev_index)
         rc = self._fast_fn(*a)
         if rc != _lib.OK:
             _lib.check(rc, "hbx_env_step")
@@ -488,16 +500,12 @@ class HologramVecEnv(_VecEnvBase):
         infos = [{} for _ in range(self.num_envs)]
         if self._readback is not None:
             self._readback.synchronize()
-        h = self._host_np
-        if h[self._row_bytes:self._row_bytes + 4].view(np.int32)[0] != 0:
+        if self._h_err[0]:
             self.state.check_error()                      # clears the word and raises
-        r = h[:8 * n].view(np.float64).copy()
-        if self.obs_format != "torch":
-            r = r.astype(np.float32)
-        t = h[17 * n:18 * n] != 0
-        tr = h[18 * n:19 * n] != 0
-        dones = t | tr
+        r = self._h_rew.copy() if self.obs_format == "torch" else self._h_rew.astype(np.float32)
+        dones = np.logical_or(self._h_term, self._h_trunc)   # the kernels write 0 / 1
         if self.auto_reset and dones.any():
+            t, tr = self._h_term != 0, self._h_trunc != 0
             done_ids = np.nonzero(dones)[0].tolist()
             term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}
             if self.obs_format != "torch":
