@@ -653,6 +653,8 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     const bool fuse_rc = to_recon && (pd.R == 32 || pd.R == 16);
     pdx.rc_pending = fuse_rc ? ed.recon_pending : nullptr;
     pdx.rc_cache = fuse_rc ? e->intensity + (size_t)b0 * G * hw : nullptr;
+    // N = 1024 / 256: the finalize kernel sums the row-block partials itself (no k_reduce_partials)
+    pdx.skip_reduce = (pd.R == 32 || pd.R == 16) ? 1 : 0;
     if (to_recon && !fuse_rc)
       HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
     HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
@@ -664,7 +666,7 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
                                           accepted ? accepted + b0 : nullptr,
                                           terminated ? terminated + b0 : nullptr,
                                           truncated ? truncated + b0 : nullptr, p->accept_flag, p->delta,
-                                          st));
+                                          st, pdx.skip_reduce ? pd.partial : nullptr, pd.N / (256 / pd.R)));
     if (group_intensity)
       HBX_HIP(hipMemcpyAsync(group_intensity + (size_t)b0 * hw, p->job_inten, (size_t)n * hw * sizeof(float),
                              hipMemcpyDeviceToDevice, st));

@@ -271,7 +271,8 @@ hipError_t launch_env_step_finalize(const JobDesc* jobs, const double* job_stats
                                     int P, int H, int W, const EnvDev& env, const EnvParams& prm,
                                     double count, int rel, double peak, double* reward, double* psnr,
                                     uint8_t* acc, uint8_t* term, uint8_t* trunc, int32_t* accept_flag,
-                                    double* delta_scratch, hipStream_t st);
+                                    double* delta_scratch, hipStream_t st,
+                                    const double* partial = nullptr, int RB = 0);
 hipError_t launch_dbs_step_finalize(const JobDesc* jobs, const double* job_stats, int n, int G, int P,
                                     int H, int W, uint64_t* mask, double* chan_stats, double* prev,
                                     double* psnr, uint8_t* acc, int rule, double count, int rel,

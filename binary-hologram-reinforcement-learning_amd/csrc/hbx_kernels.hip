@@ -152,9 +152,38 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
                                     int rel_scale, double peak, double* __restrict__ reward_out,
                                     double* __restrict__ psnr_out, uint8_t* __restrict__ acc_out,
                                     uint8_t* __restrict__ term_out, uint8_t* __restrict__ trunc_out,
-                                    int32_t* __restrict__ accept_flag, double* __restrict__ delta_out) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
+                                    int32_t* __restrict__ accept_flag, double* __restrict__ delta_out,
+                                    const double* __restrict__ partial, int RB) {
+  __shared__ double s_part[768];
+  __shared__ double s_js[3];
+  int b;
+  const double* js;
+  if (partial) {
+    // k_reduce_partials fused (one launch per step less): one wave per env sums its job's
+    // row-block partials in row-block order (k_reduce_partials' order bit for bit), lane 0
+    // finalizes
+    b = blockIdx.x;
+    const int k = threadIdx.x;
+    double acc = 0.0;
+    const double* p = partial + (size_t)b * RB * 3;
+    for (int c0 = 0; c0 < 3 * RB; c0 += 768) {
+      const int m = 3 * RB - c0 < 768 ? 3 * RB - c0 : 768;
+      for (int i = k; i < m; i += 64) s_part[i] = p[c0 + i];
+      __syncthreads();
+      if (k < 3)
+#pragma unroll 8
+        for (int i = k; i < m; i += 3) acc += s_part[i];
+      __syncthreads();
+    }
+    if (k < 3) s_js[k] = acc;
+    __syncthreads();
+    if (k != 0 || b >= n) return;
+    js = s_js;
+  } else {
+    b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n) return;
+    js = job_stats + 3 * (size_t)b;
+  }
   const JobDesc jb = jobs[b];
   if (delta_out) delta_out[b] = NAN;   // no importance lookup for an invalid job
   if (jb.env < 0) {
@@ -180,7 +209,6 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
   }
   int64_t flips = env.flip_count[b] + 1;             // env.py:167
   double* st = env.chan_stats + (size_t)b * G * 3;
-  const double* js = job_stats + 3 * (size_t)b;
   double sxy = 0.0, sxx = 0.0, syy = 0.0;
   for (int gg = 0; gg < G; ++gg) {
     if (gg == g) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
@@ -636,11 +664,11 @@ hipError_t launch_env_step_finalize(const JobDesc* jobs, const double* job_stats
                                     int P, int H, int W, const EnvDev& env, const EnvParams& prm,
                                     double count, int rel, double peak, double* reward, double* psnr,
                                     uint8_t* acc, uint8_t* term, uint8_t* trunc, int32_t* accept_flag,
-                                    double* delta_scratch, hipStream_t st) {
+                                    double* delta_scratch, hipStream_t st, const double* partial, int RB) {
   const bool imp = prm.reward_kind == 1 && reward && env.imp_changes && env.imp_values && env.imp_count > 0;
-  hipLaunchKernelGGL(k_env_step_finalize, dim3((n + 63) / 64), dim3(64), 0, st, jobs, job_stats, n,
+  hipLaunchKernelGGL(k_env_step_finalize, dim3(partial ? n : (n + 63) / 64), dim3(64), 0, st, jobs, job_stats, n,
                      G, P, H, W, env, prm, count, rel, peak, reward, psnr, acc, term, trunc,
-                     accept_flag, imp ? delta_scratch : nullptr);
+                     accept_flag, imp ? delta_scratch : nullptr, partial, RB);
   if (imp)
     hipLaunchKernelGGL(k_importance_reward, dim3(n), dim3(256), 0, st, delta_scratch, env.imp_changes,
                        env.imp_values, env.imp_count, n, reward);
