@@ -19,3 +19,6 @@ for k in 2 4 6; do
   timeout -k 10 200 python tools/dbs_walk_bench.py --flips 16384 --k $k >> $T/dbs_walk_k.txt 2>&1 || exit 23
 done
 grep device_walk $T/dbs_walk_k.txt
+# bench.py --gpus 2 with no outer launcher starts its own two ranks
+HBX_BENCH_REHEARSE_ONE_GPU=1 timeout -k 10 400 python3 bench.py --gpus 2 --steps 10 --warmup 2 > $T/rehearse_world2.json 2> $T/rehearse_world2.log || { tail -20 $T/rehearse_world2.log; exit 24; }
+cat $T/rehearse_world2.json
