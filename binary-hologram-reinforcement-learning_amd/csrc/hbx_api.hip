@@ -100,6 +100,29 @@ extern "C" {
 
 int hbx_abi_version(void) { return HBX_ABI_VERSION; }
 
+int hbx_host_alloc(size_t bytes, void** host, void** device) {
+  if (!host || !device || bytes == 0) return fail(HBX_ERR_INVALID, "hbx_host_alloc: null pointer or zero size");
+  *host = nullptr;
+  *device = nullptr;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !h)
+    return fail(HBX_ERR_NOMEM, "hipHostMalloc");
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipHostFree(h);
+    return fail(HBX_ERR_HIP, "hipHostGetDevicePointer");
+  }
+  *host = h;
+  *device = d;
+  return HBX_OK;
+}
+
+int hbx_host_free(void* host) {
+  if (!host) return HBX_OK;
+  HBX_HIP(hipHostFree(host));
+  return HBX_OK;
+}
+
 const char* hbx_last_error(void) { return g_last_error.c_str(); }
 
 int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, int32_t device) {
@@ -337,6 +360,8 @@ EnvDev env_dev(const hbx_env_buffers_t* e) {
   d.state_bytes = e->state_bytes;
   d.recon_pending = e->recon_pending;
   d.plane_slot = (e->plane_inten && e->plane_slot) ? e->plane_slot : nullptr;
+  d.error = e->error;
+  d.error_host = e->error_host;
   return d;
 }
 
@@ -639,7 +664,8 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   ep.t_psnr_diff = prm->t_psnr_diff; ep.reward_weight = prm->reward_weight;
   ep.accept_rule = prm->accept_rule;
   ep.reward_kind = prm->reward_kind;
-  const EnvDev base = env_dev(e);
+  EnvDev base = env_dev(e);
+  if (!base.error) base.error = p->err;   // the word k_jobs_from_actions sets
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
     const EnvDev ed = env_offset(base, b0, CH, G, N);

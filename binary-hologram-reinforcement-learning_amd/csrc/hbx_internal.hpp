@@ -175,6 +175,8 @@ struct EnvDev {
   int32_t* recon_pending;     // [B] group the next step reconciles (nullable; with recon)
   int32_t* plane_slot;        // [B][CH + 2] plane-cache slots (nullable, ABI v9): an accepted step
                               // swaps the flipped pair's slots with the two spares
+  const int32_t* error;       // the sticky error word (nullable)
+  int32_t* error_host;        // its mirror, written by the env-step finalize (nullable, ABI v11)
 };
 
 struct EnvParams {

@@ -184,6 +184,9 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     if (b >= n) return;
     js = job_stats + 3 * (size_t)b;
   }
+  // the error word is final here (k_jobs_from_actions, the only kernel of the step that sets it,
+  // ran before): mirror it next to the step outputs (ABI v11)
+  if (b == 0 && env.error_host) env.error_host[0] = env.error ? env.error[0] : 0;
   const JobDesc jb = jobs[b];
   if (delta_out) delta_out[b] = NAN;   // no importance lookup for an invalid job
   if (jb.env < 0) {

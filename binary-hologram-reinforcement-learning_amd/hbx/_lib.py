@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 10
+ABI_VERSION = 11
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = (
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
     "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
     "hbx_planes_fill", "hbx_eval_flips_planes", "hbx_commit_flip_planes", "hbx_dbs_walk_planes",
+    "hbx_host_alloc", "hbx_host_free",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -84,6 +85,7 @@ class EnvBuffers(C.Structure):
         ("imp_count", C.c_int32), ("reserved", C.c_int32),
         ("state_bytes", C.c_void_p), ("recon", C.c_void_p), ("recon_pending", C.c_void_p),
         ("plane_inten", C.c_void_p), ("plane_slot", C.c_void_p),   # ABI v9 plane cache
+        ("error_host", C.c_void_p),                                 # ABI v11 error mirror
     ]
 
 
@@ -131,6 +133,8 @@ def _declare(lib):
     lib.hbx_eval_flips_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I32, VP, VP, VP]
     lib.hbx_commit_flip_planes.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP, VP, I32, VP]
     lib.hbx_dbs_walk_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I64, VP, VP, VP, I64, I32, I32, VP]
+    lib.hbx_host_alloc.argtypes = [C.c_size_t, C.POINTER(VP), C.POINTER(VP)]
+    lib.hbx_host_free.argtypes = [VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_set_timing_sampled.argtypes = [VP, I32, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),

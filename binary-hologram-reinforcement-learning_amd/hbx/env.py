@@ -287,9 +287,13 @@ class HologramVecEnv(_VecEnvBase):
         self._acc, self._term, self._trunc = raw[16 * n:17 * n], raw[17 * n:18 * n], raw[18 * n:19 * n]
         self.state.error = raw[self._row_bytes:self._row_bytes + 4].view(torch.int32)   # the kernels' error word
         self.state.bufs.error = self.state.error.data_ptr()
-        self._host_raw = torch.zeros(self._row_bytes + 8, dtype=torch.uint8,
-                                     pin_memory=self.device.type == "cuda")
-        self._host_np = h = self._host_raw.numpy()
+        # the host side of the row: host-mapped memory (ABI v11) that the step kernels write
+        # directly on the common path (_fast_step), so step() reads the results without a
+        # device -> host copy; the other paths copy the device row into it
+        self._hrow = HostRow(self.plan.lib, self._row_bytes + 8)
+        self._host_t = torch.from_numpy(self._hrow.array)
+        self.state.bufs.error_host = self._hrow.device + self._row_bytes
+        self._host_np = h = self._hrow.array
         # views of the pinned row, built once: step()'s work between the readback and its return
         # is on the GPU's critical path (the next step cannot launch before it)
         self._h_rew = h[:8 * n].view(np.float64)
@@ -473,9 +477,9 @@ class HologramVecEnv(_VecEnvBase):
         if self._fast_args is None:
             p = self.plan
             self._fast_fn = p.lib.hbx_env_step
-            self._fast_args = [p._h, C.byref(self.state.bufs), C.byref(self.params), self.num_envs, None,
-                               self._reward.data_ptr(), self._psnr.data_ptr(), self._acc.data_ptr(),
-                               self._term.data_ptr(), self._trunc.data_ptr(), None, None]
+            n, d = self.num_envs, self._hrow.device   # outputs straight into the host-mapped row
+            self._fast_args = [p._h, C.byref(self.state.bufs), C.byref(self.params), n, None,
+                               d, d + 8 * n, d + 16 * n, d + 17 * n, d + 18 * n, None, None]
         self._last_actions = actions
         a = self._fast_args
         a[4] = actions.data_ptr()
@@ -490,10 +494,11 @@ class HologramVecEnv(_VecEnvBase):
         (done envs report their last observation as info["terminal_observation"])."""
         if not self._fast_step(actions):
             self.step_device(actions)
+            # the other paths write the device row: one device -> host copy (rewards, done flags,
+            # the error word), queued behind the step
+            self._host_t.copy_(self._out_raw, non_blocking=True)
         n = self.num_envs
-        # one device -> pinned host copy per step (rewards, done flags, the error word), queued
-        # behind the step; the observation views and infos are built while it is in flight
-        self._host_raw.copy_(self._out_raw, non_blocking=True)
+        # the observation views and infos are built while the step is in flight
         if self._readback is not None:
             self._readback.record()
         obs = self.observe(stepped=True)
@@ -522,6 +527,16 @@ class HologramVecEnv(_VecEnvBase):
             self.reset_envs(done_ids)
             obs = self.observe(stepped=False)
         return self._format(obs), r, dones, infos
+
+    def last_step(self) -> dict:
+        """The last step()'s per-env results as numpy arrays, copied out of the host row:
+        reward / psnr (f64), accepted / terminated / truncated (bool) -- env.py:184-259's
+        psnr_after, the rollback decision and the two done flags (step() returns reward and
+        terminated | truncated)."""
+        n, h = self.num_envs, self._host_np
+        return {"reward": self._h_rew.copy(), "psnr": h[8 * n:16 * n].view(np.float64).copy(),
+                "accepted": h[16 * n:17 * n] != 0, "terminated": self._h_term != 0,
+                "truncated": self._h_trunc != 0}
 
     # -- SB3 VecEnv surface (stable_baselines3/common/vec_env/base_vec_env.py) ---------
     def _indices(self, indices):
@@ -674,7 +689,36 @@ class HologramVecEnv(_VecEnvBase):
         return self.state.prev_psnr
 
     def close(self):
+        if self._readback is not None:
+            self._readback.synchronize()
+        self._hrow.close()
         self.plan.close()
+
+
+class HostRow:
+    """Page-locked host bytes the GPU reads and writes directly (hbx_host_alloc, ABI v11):
+    `array` is the uint8 numpy view on the CPU, `device` the address kernels take."""
+
+    def __init__(self, lib, nbytes: int):
+        h, d = C.c_void_p(), C.c_void_p()
+        rc = lib.hbx_host_alloc(nbytes, C.byref(h), C.byref(d))
+        if rc != _lib.OK:
+            _lib.check(rc, "hbx_host_alloc")
+        self._lib, self.host, self.device, self.nbytes = lib, h.value, d.value, nbytes
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(h.value))
+        self.array[:] = 0
+
+    def close(self):
+        if self.host:
+            self.array = None
+            self._lib.hbx_host_free(self.host)
+            self.host = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
 
 
 def _to_numpy(obs: dict):

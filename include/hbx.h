@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 10
+#define HBX_ABI_VERSION 11
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -137,6 +137,12 @@ typedef struct hbx_env_buffers {
   int32_t* plane_slot;     /* [B][G*P + 2] pool slot of each plane; [G*P] and
                               [G*P + 1] are the spares (caller-owned, filled
                               by reset)                                       */
+  /* ABI v11: one-copy-free step readback.  hbx_env_step's last kernel copies
+   * *error here (nullable; typically host memory from hbx_host_alloc, given by
+   * its device address), so a caller whose reward / psnr / flag outputs also
+   * live in such memory reads the whole step result on the host once the
+   * stream work is complete, with no device-to-host copy. */
+  int32_t* error_host;
 } hbx_env_buffers_t;
 
 /* BinaryHologramEnv.__init__ keyword arguments (env.py:38) + RW (env.py:29). */
@@ -155,6 +161,15 @@ typedef struct hbx_plan* hbx_plan_t;
 /* Library identity. */
 int hbx_abi_version(void);
 const char* hbx_last_error(void);
+
+/* ABI v11: page-locked host memory that the GPU reads and writes directly
+ * (mapped, coherent).  *host is the CPU address, *device the address to pass
+ * to kernels (the step outputs of hbx_env_step, env->error_host).  The
+ * reference's VecEnv hands numpy rewards / dones to SB3 every step
+ * (train-PPO.py:296-322, env.py:259): the step kernels write them here and the
+ * host reads them without a copy engine round trip.  Free with hbx_host_free. */
+int hbx_host_alloc(size_t bytes, void** host, void** device);
+int hbx_host_free(void* host);
 
 /* Plan: owns twiddles, transfer-function tables and a workspace for up to
  * `max_jobs` concurrent group propagations (P * 12 * N^2 bytes per job:

@@ -55,6 +55,13 @@ int main(void) {
   CHECK(hbx_commit_flip(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_commit_flip_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_flip_map(NULL, NULL, NULL, NULL, NULL, NULL) == HBX_ERR_INVALID);
+  {
+    void *h = (void*)1, *d = (void*)1;
+    CHECK(hbx_host_alloc(0, &h, &d) == HBX_ERR_INVALID);   /* no HIP call before the checks */
+    CHECK(h == (void*)1 && d == (void*)1);
+    CHECK(hbx_host_alloc(64, NULL, &d) == HBX_ERR_INVALID);
+    CHECK(hbx_host_free(NULL) == HBX_OK);
+  }
   CHECK(hbx_planes_fill(NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_eval_flips_planes(NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, 1, NULL, NULL, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_commit_flip_planes(NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL, NULL, 1, NULL) ==

@@ -64,7 +64,7 @@ def test_obs_mirrors_follow_steps_and_rollbacks(N, steps):
         obs, r, dones, infos = env.step(acts[k])
         assert obs["state"].data_ptr() == st.state_bytes.data_ptr()
         assert torch.equal(st.state_bytes, unpack_bits(st.mask, N)), k
-        acc = env._acc.bool()
+        acc = env.last_step()["accepted"]
         n_acc += int(acc.sum())
         n_rej += int((~acc).sum())
         if k % 20 == 0 or k == steps - 1:
@@ -239,7 +239,7 @@ def test_obs_sync_resolve_right_after_accepted_step():
         # reconcile would have restored anyway)
         assert torch.equal(env.state.recon, twin.state.recon), k
         assert torch.equal(env.state.prev_psnr, twin.state.prev_psnr), k
-        acc = env._acc.bool()
+        acc = torch.as_tensor(env.last_step()["accepted"], device="cuda")
         if acc.any() and k % 3 == 0:
             assert int(st.recon_pending[acc].min()) > 0
             plan.env_obs_sync(st.bufs, B, _lib.OBS_RECON | _lib.OBS_RESOLVE)
@@ -254,3 +254,37 @@ def test_obs_sync_resolve_right_after_accepted_step():
     plan.close()
     env.close()
     twin.close()
+
+
+@pytest.mark.parametrize("N", [256, 1024])
+def test_step_host_row_equals_device_row(N):
+    """ABI v11: step() has the step kernels write reward / psnr / flags and the error mirror
+    straight into host-mapped memory (no device -> host copy).  Against a twin stepped through
+    step_device (the device row): every result equal at every step; an out-of-range action
+    still raises through the mirrored error word, and the env steps on afterwards."""
+    import hbx
+    cfg = hbx.rgb_config(1024) if N == 1024 else hbx.mono_config(256)
+    B = 6
+    a, g = _env(cfg, B, 91)
+    b, _ = _env(cfg, B, 91)
+    a.reset()
+    b.reset()
+    acts = torch.randint(0, cfg.channels * N * N, (40, B), generator=g, device="cuda")
+    n_acc = 0
+    for k in range(40):
+        _, r, d, _ = a.step(acts[k])
+        rew, psnr, acc, term, trunc = (t.cpu().numpy() for t in b.step_device(acts[k]))
+        last = a.last_step()
+        assert np.array_equal(r, rew) and np.array_equal(last["psnr"], psnr), k
+        assert np.array_equal(last["accepted"], acc != 0), k
+        assert np.array_equal(d, (term != 0) | (trunc != 0)), k
+        n_acc += int(last["accepted"].sum())
+    assert 0 < n_acc < 40 * B
+    bad = acts[0].clone()
+    bad[2] = cfg.channels * N * N          # out of range
+    with pytest.raises(ValueError):
+        a.step(bad)
+    _, r, _, _ = a.step(acts[1])           # the word was cleared: the next step is clean
+    assert np.isfinite(r).all()
+    a.close()
+    b.close()

@@ -49,12 +49,13 @@ def test_planes_mode_bit_exact_vs_fft_mode(N, B, steps, max_steps):
         o2, r2, d2, _ = planes.step(acts[k])
         assert np.array_equal(r1, r2), k
         assert np.array_equal(d1, d2), k
-        assert torch.equal(fft._psnr, planes._psnr), k
-        assert torch.equal(fft._acc, planes._acc), k
+        l1, l2 = fft.last_step(), planes.last_step()
+        assert np.array_equal(l1["psnr"], l2["psnr"]), k
+        assert np.array_equal(l1["accepted"], l2["accepted"]), k
         assert torch.equal(o1["recon_image"], o2["recon_image"]), k      # stepped (pre-rollback) group too
         assert torch.equal(o1["state"], o2["state"]), k
-        n_acc += int(fft._acc.sum())
-        n_rej += int((1 - fft._acc).sum())
+        n_acc += int(l1["accepted"].sum())
+        n_rej += int((~l1["accepted"]).sum())
         n_done += int(np.sum(d1))
         if k % 30 == 0 or k == steps - 1:
             _same_state(fft, planes, k)
