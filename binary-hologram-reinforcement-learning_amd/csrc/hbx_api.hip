@@ -692,7 +692,8 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
                                           accepted ? accepted + b0 : nullptr,
                                           terminated ? terminated + b0 : nullptr,
                                           truncated ? truncated + b0 : nullptr, p->accept_flag, p->delta,
-                                          st, pdx.skip_reduce ? pd.partial : nullptr, pd.N / (256 / pd.R)));
+                                          st, pdx.skip_reduce ? pd.partial : nullptr,
+                                          pdx.skip_reduce ? pd.N / (256 / pd.R) : 0));
     if (group_intensity)
       HBX_HIP(hipMemcpyAsync(group_intensity + (size_t)b0 * hw, p->job_inten, (size_t)n * hw * sizeof(float),
                              hipMemcpyDeviceToDevice, st));
