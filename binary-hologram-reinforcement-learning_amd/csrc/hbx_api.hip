@@ -683,7 +683,12 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     pdx.skip_reduce = (pd.R == 32 || pd.R == 16) ? 1 : 0;
     if (to_recon && !fuse_rc)
       HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
-    HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
+    if (pdx.skip_reduce) {     // N = 1024 / 256: the first pass decodes the actions itself
+      pdx.actions = actions + b0;
+      pdx.act_err = e->error ? e->error : p->err;
+    } else {
+      HBX_HIP(hbx::launch_jobs_from_actions(actions + b0, n, N, N, P, CH, p->jobs, e->error ? e->error : p->err, st));
+    }
     HBX_HIP(hbx::run_jobs(pdx, p->jobs, n, reinterpret_cast<const uint32_t*>(ed.mask), ed.target,
                           to_recon ? rec : (want_inten ? p->job_inten : nullptr), nullptr, st));
     HBX_HIP(hbx::launch_env_step_finalize(p->jobs, pd.job_stats, n, G, P, N, N, ed, ep, pixel_count(p),

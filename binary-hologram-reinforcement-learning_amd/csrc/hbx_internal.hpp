@@ -40,6 +40,22 @@ struct JobDesc {
   int32_t flip_pix;    // row * W + col
 };
 
+// env.py:157-161: action -> (channel, pixel) of env b; an action outside [0, CH*hw) is an
+// invalid job (env -1).  Shared by k_jobs_from_actions and the first pass's fused decode.
+__host__ __device__ __forceinline__ JobDesc job_of_action(int64_t a, int b, int64_t hw, int P, int CH) {
+  JobDesc jd;
+  if (a < 0 || a >= (int64_t)CH * hw) {
+    jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
+  } else {
+    const int ch = (int)(a / hw);
+    jd.env = b;
+    jd.group = ch / P;
+    jd.flip_plane = ch % P;
+    jd.flip_pix = (int)(a % hw);
+  }
+  return jd;
+}
+
 // Intermediate layout of the fused N = R^2 path (hbx_passes.hip).  The row
 // passes run blocks of row_nt(R) = 256 threads = panel_rows(R) rows; a plane of
 // L lines is stored as N / PAN panels [L][PAN], panel q at q * PAN * L.  A is
@@ -150,6 +166,10 @@ struct PlanDev {
   const int32_t* rc_pending; // [env] nullable
   float* rc_cache;           // [env][G][N][N] the intensity cache
   int skip_reduce = 0;       // 1: leave the per-row-block partials (a caller reduces them itself)
+  // env step at N = 1024 / 256: the first pass decodes the actions itself (no k_jobs_from_actions
+  // launch) and one of its workgroups per job writes the JobDesc the later passes read
+  const int64_t* actions = nullptr;
+  int32_t* act_err = nullptr;
 };
 constexpr int kPlanesOff = 0, kPlanesFill = 1, kPlanesStep = 2;
 

@@ -21,19 +21,8 @@ __global__ void k_jobs_from_actions(const int64_t* __restrict__ actions, int n, 
                                     int32_t* __restrict__ err) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n) return;
-  const int64_t a = actions[b];
-  const int64_t hw = (int64_t)H * W;
-  JobDesc jd;
-  if (a < 0 || a >= (int64_t)CH * hw) {
-    jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
-    if (err) atomicOr(err, 1);
-  } else {
-    const int ch = (int)(a / hw);
-    jd.env = b;
-    jd.group = ch / P;
-    jd.flip_plane = ch % P;
-    jd.flip_pix = (int)(a % hw);
-  }
+  const JobDesc jd = job_of_action(actions[b], b, (int64_t)H * W, P, CH);
+  if (jd.env < 0 && err) atomicOr(err, 1);
   jobs[b] = jd;
 }
 

@@ -109,12 +109,27 @@ template <int R>
 constexpr int rowfwd_iters() { return R == 32 ? 4 : (R == 16 ? 2 : 1); }   // N = 256: 2 (r03,
 // with nt A stores: 0.0634 -> 0.0585 ms; 4 row blocks 0.0611)
 
+// The job of workgroup's job index j: jobs[j], or (actions non-null: the env step) decoded from
+// actions[j] here, the workgroup with rbw = 0 of the job's first pair writing it to jobs[j] for
+// the later passes and flagging an invalid action in *err
+__device__ __forceinline__ JobDesc first_pass_job(const JobDesc* jobs, const int64_t* actions, int32_t* err,
+                                                  int j, bool writer, int64_t hw, int P, int CH) {
+  if (!actions) return jobs[j];
+  const JobDesc jb = job_of_action(actions[j], j, hw, P, CH);
+  if (writer && threadIdx.x == 0) {
+    const_cast<JobDesc*>(jobs)[j] = jb;
+    if (jb.env < 0 && err) atomicOr(err, 1);
+  }
+  return jb;
+}
+
 template <int R, int NT, int SK, int RIT = rowfwd_iters<R>()>
-__global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restrict__ jobs,
+__global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
                                                    const uint32_t* __restrict__ mask,
                                                    float2* __restrict__ ws_a,
                                                    const float2* __restrict__ tw_glob, int P,
-                                                   int CH, float va, float vb, int pair_step) {
+                                                   int CH, float va, float vb, int pair_step,
+                                                   const int64_t* __restrict__ actions, int32_t* err) {
   constexpr int N = R * R;
   constexpr int GPB = NT / R;          // rows per row block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
@@ -135,7 +150,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
   bid /= RBW;
   const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
   const int j = bid / npair;
-  const JobDesc jb = jobs[j];
+  const JobDesc jb = first_pass_job(jobs, actions, err, j, rbw == 0 && bid % npair == 0, (int64_t)N * N, P, CH);
   if (jb.env < 0) return;  // uniform per block
   const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
@@ -240,11 +255,12 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* __restri
 //    through a 32-KB tile that aliases those FFT tiles: 8 KB twiddles + 33.8 KB.
 // Same arithmetic as k_rowfwd, so the A it writes is bit-identical.
 template <int SK, int RIT = rowfwd_iters<32>()>
-__global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__ jobs,
+__global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
                                                      const uint32_t* __restrict__ mask,
                                                      float2* __restrict__ ws_a,
                                                      const float2* __restrict__ tw_glob, int P, int CH,
-                                                     float va, float vb, int pair_step) {
+                                                     float va, float vb, int pair_step,
+                                                     const int64_t* __restrict__ actions, int32_t* err) {
   constexpr int R = 32, NT = 256, N = R * R;
   constexpr int GPB = NT / R;          // 8 rows per row block
   constexpr int WPR = N / 32;          // 32 mask words per row = one per lane
@@ -265,7 +281,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* __restrict__
   bid /= RBW;
   const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
   const int j = bid / npair;
-  const JobDesc jb = jobs[j];
+  const JobDesc jb = first_pass_job(jobs, actions, err, j, rbw == 0 && bid % npair == 0, (int64_t)N * N, P, CH);
   if (jb.env < 0) return;  // uniform per block
   const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
@@ -1003,20 +1019,20 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if constexpr (R == 32) {
       if (small)
         hipLaunchKernelGGL((k_rowfwd32<SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(256), 0, st, jobs, mask,
-                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
       else
         hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(rf_blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
-                           pd.va, pd.vb, pair);
+                           pd.va, pd.vb, pair, pd.actions, pd.act_err);
     } else if constexpr (kTiledB<R>) {
       if (small)
         hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(kRowNT<R>), 0,
-                           st, jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+                           st, jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
       else
         hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask,
-                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
     } else {
       hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a,
-                         pd.tw, P, CH, pd.va, pd.vb, pair);
+                         pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
     }
     if (tm) tm->end(0, n_jobs, st);
   }
