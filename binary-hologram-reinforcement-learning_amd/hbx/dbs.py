@@ -377,13 +377,13 @@ def planes_visited(q: float, k: int, groups: int) -> float:
     return vis
 
 
-def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0: float = 140.0,
-                  c: float = 16.0, fill: int = 8) -> int:
+def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0: float = 62.0,
+                  c: float = 15.0, fill: int = 2) -> int:
     """Speculation depth of the FFT-mode plane-cached walk for acceptance rate q: K minimising
-    the batch time / expected candidates visited (planes_visited), with the batch time t0 (us,
-    the latency of a few-job launch sequence, measured ~147 us at 1024 x 24) until K exceeds
-    `fill` candidates and c us per candidate beyond (a 128-job plane-cached step is 2.08 ms =
-    16 us per candidate)."""
+    the batch time / expected candidates visited (planes_visited), with the batch time t0 (us)
+    up to `fill` candidates and c us per candidate beyond.  Fit to the device walk's batches at
+    1024 x 24 (tools/dbs_walk_bench.py, profiles/r04/dbs_walk_k_r04f.txt: K = 2, 4, 6, 8 ->
+    62, 87, 127, 152 us per batch); at q = 0.5 it picks K = 3."""
     q = min(max(q, 1e-6), 1.0)
     best, bk = math.inf, k_min
     for k in range(max(1, k_min), max(k_min, k_max) + 1):
