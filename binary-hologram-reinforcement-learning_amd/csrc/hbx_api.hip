@@ -525,8 +525,19 @@ int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, co
   int rc = check_plan(p);
   if (rc) return rc;
   if (!e) return fail(HBX_ERR_INVALID, "null env buffers");
+  if (what == HBX_OBS_SETTLE) {
+    if (!e->recon || !e->intensity || !e->recon_pending)
+      return fail(HBX_ERR_INVALID, "HBX_OBS_SETTLE needs recon, intensity and recon_pending");
+    if (n_env < 0) return fail(HBX_ERR_INVALID, "n_env");
+    const int n = env_ids ? n_ids : n_env;
+    if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_ids");
+    HBX_HIP(hipSetDevice(p->device));
+    HBX_HIP(hbx::launch_obs_settle(env_ids, n, e->intensity, e->recon, e->recon_pending, p->pd.G,
+                                   (size_t)p->pd.N * p->pd.N, (hipStream_t)stream));
+    return HBX_OK;
+  }
   if (what & ~(HBX_OBS_STATE | HBX_OBS_RECON | HBX_OBS_RESOLVE))
-    return fail(HBX_ERR_INVALID, "what: HBX_OBS_STATE | HBX_OBS_RECON | HBX_OBS_RESOLVE");
+    return fail(HBX_ERR_INVALID, "what: HBX_OBS_STATE | HBX_OBS_RECON | HBX_OBS_RESOLVE, or HBX_OBS_SETTLE alone");
   if ((what & HBX_OBS_RESOLVE) && !(what & HBX_OBS_RECON))
     return fail(HBX_ERR_INVALID, "HBX_OBS_RESOLVE is a modifier of HBX_OBS_RECON");
   const bool st_on = (what & HBX_OBS_STATE) != 0, rc_on = (what & HBX_OBS_RECON) != 0;

@@ -324,5 +324,7 @@ hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* sl
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
                            float* intensity, float* recon, int32_t* pending, int resolve, int CH, int G, size_t hw,
                            hipStream_t st);
+hipError_t launch_obs_settle(const int32_t* env_ids, int n_ids, float* intensity, const float* recon,
+                             int32_t* pending, int G, size_t hw, hipStream_t st);
 
 }  // namespace hbx

@@ -605,6 +605,27 @@ __global__ void k_obs_sync(const int32_t* __restrict__ env_ids, const uint64_t* 
     }
   }
 }
+// HBX_OBS_SETTLE: an accepted last step's group recon -> intensity (recon untouched); then
+// k_pending_settled clears those pendings (a separate launch: every block of k_obs_settle reads
+// the pending word first).  grid (x, n_ids)
+__global__ void k_obs_settle(const int32_t* __restrict__ env_ids, float* __restrict__ intensity,
+                             const float* __restrict__ recon, const int32_t* __restrict__ pending, int G,
+                             size_t hw) {
+  const int e = env_ids ? env_ids[blockIdx.y] : (int)blockIdx.y;
+  const int p = pending[e];
+  if (p <= 0) return;
+  const size_t off = ((size_t)e * G + (p - 1)) * hw / 4;
+  const float4* src = reinterpret_cast<const float4*>(recon) + off;
+  float4* dst = reinterpret_cast<float4*>(intensity) + off;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < hw / 4; k += (size_t)gridDim.x * blockDim.x)
+    dst[k] = src[k];
+}
+__global__ void k_pending_settled(const int32_t* __restrict__ env_ids, int n_ids, int32_t* __restrict__ pending) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ids) return;
+  const int e = env_ids ? env_ids[i] : i;
+  if (pending[e] > 0) pending[e] = 0;
+}
 __global__ void k_pending_clear(const int32_t* __restrict__ env_ids, int n_ids, int32_t* __restrict__ pending) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n_ids) pending[env_ids ? env_ids[i] : i] = 0;
@@ -730,6 +751,14 @@ hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* ma
                      pending, resolve, CH, G, hw);
   if (recon && pending)
     hipLaunchKernelGGL(k_pending_clear, dim3((n_ids + 255) / 256), dim3(256), 0, st, env_ids, n_ids, pending);
+  return hipGetLastError();
+}
+hipError_t launch_obs_settle(const int32_t* env_ids, int n_ids, float* intensity, const float* recon,
+                             int32_t* pending, int G, size_t hw, hipStream_t st) {
+  if (n_ids <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)std::min<size_t>(32, (hw / 4 + 255) / 256);
+  hipLaunchKernelGGL(k_obs_settle, dim3(gx, n_ids), dim3(256), 0, st, env_ids, intensity, recon, pending, G, hw);
+  hipLaunchKernelGGL(k_pending_settled, dim3((n_ids + 255) / 256), dim3(256), 0, st, env_ids, n_ids, pending);
   return hipGetLastError();
 }
 hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, double count, int rel,

@@ -25,7 +25,7 @@ MAX_GROUPS = 4
 WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
 WALK_FUSED_K = (1, 2, 3, 4)   # one launch per batch (two accepts resolved for K = 2..4)
 PRECISION_F32, PRECISION_BF16_STORE, PRECISION_F16_STORE = 0, 1, 2   # hbx_plan_set_precision
-OBS_STATE, OBS_RECON, OBS_RESOLVE = 1, 2, 4   # hbx_env_obs_sync
+OBS_STATE, OBS_RECON, OBS_RESOLVE, OBS_SETTLE = 1, 2, 4, 8   # hbx_env_obs_sync
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",

@@ -304,6 +304,7 @@ class HologramVecEnv(_VecEnvBase):
         self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
         self._fast_args = None
+        self._settle_args = None
         self._obs_views = None
         self.episode_count = 0
         if HAVE_SB3:  # pragma: no cover - SB3 absent here
@@ -489,6 +490,21 @@ class HologramVecEnv(_VecEnvBase):
             _lib.check(rc, "hbx_env_step")
         return True
 
+    def _settle(self):
+        """HBX_OBS_SETTLE queued behind the readback event: the accepted envs' stepped group goes
+        recon -> intensity cache while the host turns the step around (the next step's k_rowinv
+        would otherwise do that copy on the critical path); recon, the returned observation,
+        is not touched."""
+        if self._settle_args is None:
+            p = self.plan
+            self._settle_fn = p.lib.hbx_env_obs_sync
+            self._settle_args = [p._h, C.byref(self.state.bufs), self.num_envs, None, 0, _lib.OBS_SETTLE, None]
+        a = self._settle_args
+        a[6] = _raw_stream(self._dev_index)
+        rc = self._settle_fn(*a)
+        if rc != _lib.OK:
+            _lib.check(rc, "hbx_env_obs_sync(SETTLE)")
+
     def step(self, actions):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
         (done envs report their last observation as info["terminal_observation"])."""
@@ -501,6 +517,8 @@ class HologramVecEnv(_VecEnvBase):
         # the observation views and infos are built while the step is in flight
         if self._readback is not None:
             self._readback.record()
+            if self.state.recon is not None and self.mode != "psf":
+                self._settle()
         obs = self.observe(stepped=True)
         infos = [{} for _ in range(self.num_envs)]
         ev = self._readback

@@ -428,11 +428,19 @@ int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_en
  *                  intensity lives in recon only (recon_pending = group + 1), so that
  *                  group goes recon -> intensity and the others intensity -> recon.
  *                  Use it to re-sync mid-episode without rewriting intensity.
+ *   HBX_OBS_SETTLE (ABI v11, alone) the accepted half of that reconcile only: envs
+ *                  whose last step was accepted (recon_pending > 0) copy the stepped
+ *                  group recon -> intensity and clear recon_pending; recon is not
+ *                  touched (it is still the observation the step returned), rolled-back
+ *                  envs keep their pending restore for the next step.  A VecEnv queues
+ *                  it right behind the step's readback, so the copy runs while the host
+ *                  turns the step around instead of inside the next step's k_rowinv.
  * hbx_env_reset does both for the envs it resets; a caller that restores
  * masks or intensities by itself (checkpoint load) calls it after. */
 #define HBX_OBS_STATE 1
 #define HBX_OBS_RECON 2
 #define HBX_OBS_RESOLVE 4
+#define HBX_OBS_SETTLE 8
 int hbx_env_obs_sync(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
                      const int32_t* env_ids, int32_t n_ids, int32_t what, void* stream);
 

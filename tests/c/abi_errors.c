@@ -67,6 +67,7 @@ int main(void) {
   CHECK(hbx_commit_flip_planes(NULL, NULL, NULL, NULL, NULL, 1, NULL, NULL, NULL, NULL, 1, NULL) ==
         HBX_ERR_INVALID);
   CHECK(hbx_env_obs_sync(NULL, NULL, 0, NULL, 0, HBX_OBS_RECON | HBX_OBS_RESOLVE, NULL) == HBX_ERR_INVALID);
+  CHECK(hbx_env_obs_sync(NULL, NULL, 0, NULL, 0, HBX_OBS_SETTLE, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_dbs_walk_planes(NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL) ==
         HBX_ERR_INVALID);
   CHECK(hbx_dbs_walk_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL) ==

@@ -233,13 +233,15 @@ def test_obs_sync_resolve_right_after_accepted_step():
     acts = torch.randint(0, cfg.channels * 256 * 256, (40, B), generator=g, device="cuda")
     synced = 0
     for k in range(40):
-        env.step(acts[k])
-        twin.step(acts[k])
+        # step_device: VecEnv.step settles accepted steps itself (HBX_OBS_SETTLE), this test
+        # wants the pending reconcile an accepted step leaves behind
+        env.step_device(acts[k])
+        twin.step_device(acts[k])
         # the two agree after every step (a re-sync only changes what the previous step's
         # reconcile would have restored anyway)
         assert torch.equal(env.state.recon, twin.state.recon), k
         assert torch.equal(env.state.prev_psnr, twin.state.prev_psnr), k
-        acc = torch.as_tensor(env.last_step()["accepted"], device="cuda")
+        acc = env._acc.bool()
         if acc.any() and k % 3 == 0:
             assert int(st.recon_pending[acc].min()) > 0
             plan.env_obs_sync(st.bufs, B, _lib.OBS_RECON | _lib.OBS_RESOLVE)
@@ -288,3 +290,42 @@ def test_step_host_row_equals_device_row(N):
     assert np.isfinite(r).all()
     a.close()
     b.close()
+
+
+def test_step_settles_accepted_groups():
+    """VecEnv.step queues HBX_OBS_SETTLE behind its readback (ABI v11): after every step the
+    accepted envs' intensity cache already holds the stepped group (= recon) with recon_pending
+    cleared, rolled-back envs keep -(g + 1) and their cache; recon, the returned observation, is
+    the stepped intensity either way, and the env steps exactly like a twin driven through
+    step_device (which leaves the reconcile to the next step's k_rowinv)."""
+    import hbx
+    cfg = hbx.rgb_config(1024)
+    B = 4
+    env, g = _env(cfg, B, 29)
+    twin, _ = _env(cfg, B, 29)
+    env.reset()
+    twin.reset()
+    st = env.state
+    acts = torch.randint(0, cfg.channels * 1024 * 1024, (60, B), generator=g, device="cuda")
+    n_acc = n_rej = 0
+    for k in range(60):
+        before = st.intensity.clone()
+        obs, _, _, _ = env.step(acts[k])
+        twin.step_device(acts[k])
+        acc = env.last_step()["accepted"]
+        gidx = ((acts[k] // (1024 * 1024)) // cfg.planes).tolist()
+        for b in range(B):
+            gb = int(gidx[b])
+            if acc[b]:
+                n_acc += 1
+                assert int(st.recon_pending[b]) == 0, (k, b)
+                assert torch.equal(st.intensity[b, gb], st.recon[b, gb]), (k, b)
+            else:
+                n_rej += 1
+                assert int(st.recon_pending[b]) == -(gb + 1), (k, b)
+                assert torch.equal(st.intensity[b], before[b]), (k, b)
+        assert torch.equal(obs["recon_image"][:, 0], twin.state.recon), k
+        assert torch.equal(st.prev_psnr, twin.state.prev_psnr), k
+    assert n_acc > 0 and n_rej > 0
+    env.close()
+    twin.close()
