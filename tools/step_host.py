@@ -46,6 +46,7 @@ def main():
         obs = vec.observe(stepped=True)
         infos = [{} for _ in range(B)]
         ev.record()
+        vec._settle()
         t2 = ns()
         q = 0
         while not ev.query():
