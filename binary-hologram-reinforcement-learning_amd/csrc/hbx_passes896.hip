@@ -88,7 +88,15 @@ __device__ __forceinline__ int tile896_pos(int kx, int r) {
   return kx * kGPB + (r ^ ((((m >> 2) & 7) ^ (((m >> 1) & 1) * 5)) & 7));
 }
 
+#if defined(HBX_RIT896_2)
+constexpr int kRit896 = 2;
+#elif defined(HBX_RIT896_7)
+constexpr int kRit896 = 7;
+#elif defined(HBX_RIT896_8)
+constexpr int kRit896 = 8;
+#else
 constexpr int kRit896 = 4;                       // row blocks per workgroup (112 / 4 = 28 per pair)
+#endif
 static_assert(kRB % kRit896 == 0, "row-block walk");
 
 __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict__ jobs,

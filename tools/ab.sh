@@ -13,5 +13,7 @@ for lib in "$@"; do
   HBX_LIB=$PWD/$L/$lib.so timeout -k 10 300 python bench.py $Q > gpurun_out/$T/${i}_${lib}.json 2> gpurun_out/$T/${i}_${lib}.err || exit 1
   python -c "
 import json; d = json.loads(open('gpurun_out/$T/${i}_${lib}.json').read().splitlines()[-1])
-print('%-30s %9.0f' % ('$lib', d['value']), ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in d['passes'].items()))"
+c = d.get('crop_896', {})
+print('%-30s %9.0f' % ('$lib', d['value']), ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in d['passes'].items()),
+      '| crop %.0f' % c.get('value', 0), ' '.join('%s %.3f' % (k, v['avg_ms']) for k, v in c.get('passes', {}).items()))"
 done

@@ -12,3 +12,5 @@ cat $T/step_host.txt
 timeout -k 10 200 python tools/obs_cost.py 256 > $T/obs_cost.txt 2>&1 || exit 21
 timeout -k 10 200 python tools/obs_cost.py 1024 >> $T/obs_cost.txt 2>&1 || exit 22
 grep -v amdgpu.ids $T/obs_cost.txt
+# k_rowfwd896 row blocks per workgroup (k_rowfwd896 >= 0.6 of 8 TB/s)
+bash tools/ab.sh r04g_ab libhbx libhbx_exp_RIT896_2 libhbx_exp_RIT896_7 libhbx_exp_RIT896_8 libhbx || exit 23
