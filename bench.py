@@ -202,6 +202,10 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
            "psnr_gain_db": round(res.final_psnr - res.initial_psnr, 6),
            "full_sweep_extrapolated_s": round(CH * N * N / rate, 1),
            "plane_cache": True,
+           "walk": "device-decided (hbx_dbs_walk_planes): per batch the three passes over K candidates' "
+                   "flipped pairs + one single-block decision kernel that commits up to G accepts "
+                   "(candidates of colour groups no earlier accept of the batch touched); K from the "
+                   "running acceptance rate (hbx.dbs.walk_k_planes)",
            "note": "FFT mode, speculative first-improving batches (serial accept sequence), "
                    "prefix of the shuffled order; acceptance is highest at the start of a sweep, "
                    "so the extrapolation is pessimistic.  Candidates propagate only the flipped "
