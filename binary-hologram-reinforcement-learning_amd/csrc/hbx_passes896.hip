@@ -88,15 +88,9 @@ __device__ __forceinline__ int tile896_pos(int kx, int r) {
   return kx * kGPB + (r ^ ((((m >> 2) & 7) ^ (((m >> 1) & 1) * 5)) & 7));
 }
 
-#if defined(HBX_RIT896_2)
-constexpr int kRit896 = 2;
-#elif defined(HBX_RIT896_7)
-constexpr int kRit896 = 7;
-#elif defined(HBX_RIT896_8)
+// row blocks per workgroup (112 / 8 = 14 per pair).  r04 A/B (profiles/r04/rit896_ab_r04g.txt,
+// crop k_rowfwd896 per 128-job launch): 2 -> 0.731 ms, 4 -> 0.728-0.731, 7 -> 0.711, 8 -> 0.704
 constexpr int kRit896 = 8;
-#else
-constexpr int kRit896 = 4;                       // row blocks per workgroup (112 / 4 = 28 per pair)
-#endif
 static_assert(kRB % kRit896 == 0, "row-block walk");
 
 __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict__ jobs,

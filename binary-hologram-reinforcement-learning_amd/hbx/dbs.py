@@ -385,11 +385,26 @@ def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0
     1024 x 24 (tools/dbs_walk_bench.py, profiles/r04/dbs_walk_k_r04f.txt: K = 2, 4, 6, 8 ->
     62, 87, 127, 152 us per batch); at q = 0.5 it picks K = 3."""
     q = min(max(q, 1e-6), 1.0)
+    # one pass of planes_visited's recursion gives the visited count of every k (the host runs
+    # this once per 64-batch chunk: the per-k recomputation, O(k_max^2), took ~12 ms at k_max =
+    # 256 and starved the GPU, 260 vs 78 us per batch, profiles/r04/walk_kmax_r04i.txt)
     best, bk = math.inf, k_min
-    for k in range(max(1, k_min), max(k_min, k_max) + 1):
-        cost = (t0 + c * max(0, k - fill)) / planes_visited(q, k, groups)
-        if cost < best:
-            best, bk = cost, k
+    dist = [1.0] + [0.0] * groups
+    vis = 0.0
+    for k in range(1, max(k_min, k_max) + 1):
+        nxt = [0.0] * (groups + 1)
+        for m, pm in enumerate(dist):
+            if pm:
+                cont = pm * (1.0 - m / groups)
+                vis += cont
+                nxt[m] += cont * (1.0 - q)
+                if m < groups:
+                    nxt[m + 1] += cont * q
+        dist = nxt
+        if k >= max(1, k_min):
+            cost = (t0 + c * max(0, k - fill)) / vis
+            if cost < best:
+                best, bk = cost, k
     return bk
 
 
