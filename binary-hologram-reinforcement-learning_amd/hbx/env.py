@@ -521,14 +521,10 @@ class HologramVecEnv(_VecEnvBase):
                 self._settle()
         obs = self.observe(stepped=True)
         infos = [{} for _ in range(self.num_envs)]
-        ev = self._readback
-        if ev is not None:
-            # spin on the event: a blocking HIP wait falls asleep on an interrupt after a short
-            # active phase and wakes ~20 us after the copy lands (r04e step timeline: 28 us idle
-            # between the readback and the next step's first kernel), all of it on the GPU's
-            # critical path, since the next step cannot launch before this one returns
-            while not ev.query():
-                pass
+        if self._readback is not None:
+            # a blocking wait: spinning on ev.query() measured no faster (0.3303 vs 0.3276 ms per
+            # 256x8 step, profiles/r04/step_host_r04g.txt) and would burn a core
+            self._readback.synchronize()
         if self._h_err[0]:
             self.state.check_error()                      # clears the word and raises
         r = self._h_rew.copy() if self.obs_format == "torch" else self._h_rew.astype(np.float32)
