@@ -66,11 +66,13 @@ def main():
           "  ".join(f"{k} {med(v):.1f}" for k, v in rec.items()) + f"  queries {np.median(nq):.0f}")
 
     # 2. the real step() back to back, and with a blocking wait instead of the spin
-    for label in ("step() spin", "step() event.synchronize"):
-        if "synchronize" in label:
-            orig = ev.query
-            ev_sync = ev.synchronize
-            vec._readback = type("E", (), {"record": ev.record, "query": lambda self: (ev_sync(), True)[1]})()
+    for label in ("step() event.synchronize", "step() spin on query"):
+        if "spin" in label:
+            def spin():
+                while not ev.query():
+                    pass
+            vec._readback = type("E", (), {"record": ev.record, "query": ev.query,
+                                           "synchronize": lambda self: spin()})()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(S):
