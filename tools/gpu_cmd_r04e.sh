@@ -20,3 +20,5 @@ python3 tools/step_gap.py --summarize $T/step_trace > $T/step_gaps.txt 2>&1
 python3 tools/step_gap.py --gaps $T/step_trace >> $T/step_gaps.txt 2>&1
 cat $T/step_gaps.txt
 find $T/step_trace -name "*.csv" -delete
+timeout -k 10 300 python tools/obs_cost.py > $T/obs_cost.txt 2>&1 || exit 23
+cat $T/obs_cost.txt

@@ -16,3 +16,13 @@ import json; d = json.loads(open('$T/bench.json').read().splitlines()[-1])
 print('headline', d['value'], d['roofline']['frac'], {k: v['avg_ms'] for k, v in d['passes'].items()})
 print('dbs', d.get('dbs_greedy', {}).get('flips_per_s'), 'crop', d.get('crop_896', {}).get('value'), {k: v['avg_ms'] for k, v in d.get('crop_896', {}).get('passes', {}).items()})
 m = d.get('ppo_mono_256', {}); print('mono', m.get('value'), 'obs', m.get('vecenv_step_obs', {}).get('obs_overhead_frac'))"
+# per-kernel durations of the adaptive FFT-mode walk (16,384 candidates)
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $T/walk_trace -o run -- python3 tools/dbs_walk_bench.py --flips 16384 --trace > $T/walk_trace.log 2>&1 || exit 31
+python3 - <<'PY'
+import csv, glob
+for f in glob.glob("gpurun_out/r04j/walk_trace/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print("%-60s %8s %10.2f us" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e3))
+PY
+python3 tools/step_gap.py --gaps gpurun_out/r04j/walk_trace > $T/walk_gaps.txt 2>&1; head -12 $T/walk_gaps.txt
+find $T/walk_trace -name "*trace.csv" -delete
