@@ -432,43 +432,64 @@ def cpu_baseline_mono(n_steps: int, N: int = 256):
                       f"(oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
 
 
-def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=False):
+def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=False, reps=3):
     """The step an SB3 learner calls (train-PPO.py:296-322): HologramVecEnv.step with all
     five observation keys (env.py:176-181) as device tensors, rewards / dones to the host,
     every step.  The observations are views of buffers the step kernels keep current
-    (ABI v8), so the difference to the bare device step is the recon reconcile copy, the
-    per-step host sync and the Python VecEnv bookkeeping."""
+    (ABI v8), so the difference to the bare device step is the recon write, the per-step host
+    round trip and the Python VecEnv bookkeeping.  `reps` timed runs of `steps` steps each,
+    alternating with the same number of bare device steps (step_device of an env without
+    observations, no pass timing, no metric gather) on a twin env; medians of both."""
+    import statistics
     import torch
     from hbx.env import OBS_KEYS, HologramVecEnv
     vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format="torch",
                          auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0,
                          graph=graph)
+    pure = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=(), auto_reset=False,
+                          max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0)
     vec.reset()
+    pure.reset()
     gen = torch.Generator(device="cuda").manual_seed(seed)
     n_pix = mcfg.channels * mcfg.height * mcfg.width
     actions = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda", dtype=torch.int64)
     for k in range(warmup):
         vec.step(actions[k])
+        pure.step_device(actions[k])
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(warmup, warmup + steps):
-        obs, rew, dones, infos = vec.step(actions[k])
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    t_obs, t_pure = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for k in range(warmup, warmup + steps):
+            obs, rew, dones, infos = vec.step(actions[k])
+        torch.cuda.synchronize()
+        t_obs.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        for k in range(warmup, warmup + steps):
+            pure.step_device(actions[k])
+        torch.cuda.synchronize()
+        t_pure.append(time.perf_counter() - t0)
+    dt = statistics.median(t_obs)
+    pure_ms = statistics.median(t_pure) / steps * 1e3
+    pure.close()
     shapes = {k: list(v.shape) for k, v in obs.items()}
     views = all(v.data_ptr() == getattr(vec.state, a).data_ptr() for k, v, a in
                 ((k, obs[k], {"state_record": "record", "state": "state_bytes", "pre_model": "pre_model",
                               "recon_image": "recon", "target_image": "target"}[k]) for k in obs))
     vec.close()
     ms = dt / steps * 1e3
-    return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps,
+    return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps, "reps": reps,
             "graph": graph, "ms_per_step": round(ms, 4), "bare_step_ms": round(bare_ms, 4),
-            "obs_overhead_frac": round(ms / bare_ms - 1.0, 4), "obs_keys": list(obs.keys()),
-            "obs_shapes": shapes, "obs_are_views": views,
+            "obs_overhead_frac": round(ms / bare_ms - 1.0, 4),
+            "pure_device_step_ms": round(pure_ms, 4), "overhead_vs_pure_device_step": round(ms / pure_ms - 1.0, 4),
+            "obs_keys": list(obs.keys()), "obs_shapes": shapes, "obs_are_views": views,
             "note": "HologramVecEnv.step (SB3 VecEnv surface, obs_format='torch', auto_reset on): all five "
                     "observation keys returned as views of device buffers the step kernels keep current "
-                    "(state as int8, stepped pre-rollback recon_image), rewards / dones copied to the host "
-                    "each step; bare_step_ms is the same workload's step_device without observations"}
+                    "(state as int8, stepped pre-rollback recon_image), rewards / dones / error word written "
+                    "by the step kernels into host-mapped memory; median of `reps` runs.  bare_step_ms is the "
+                    "ppo_mono_256 line's device step (same measurement as the headline: sampled pass timing "
+                    "and the per-8-step metric gather included); pure_device_step_ms is step_device of a twin "
+                    "env without observations, timing or gather, alternated with the VecEnv runs"}
 
 
 def psnr_check(vec, N):
@@ -816,11 +837,11 @@ def main():
                         "128 envs per GPU, FFT mode, same env semantics as the headline"}
             if not args.no_obs:
                 out["ppo_mono_256"]["vecenv_step_obs"] = vecenv_step_obs(
-                    mono, B, args.steps, args.warmup,
+                    mono, B, msteps, args.warmup,
                     lambda i: target_source(i)[:1, :256, :256].contiguous(),
                     lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12)
                 out["ppo_mono_256"]["vecenv_step_obs"]["graph_replay"] = {k: v for k, v in vecenv_step_obs(
-                    mono, B, 4 * args.steps, args.warmup,
+                    mono, B, msteps, args.warmup,
                     lambda i: target_source(i)[:1, :256, :256].contiguous(),
                     lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12,
                     graph=True).items() if k in ("value", "ms_per_step", "obs_overhead_frac")}
