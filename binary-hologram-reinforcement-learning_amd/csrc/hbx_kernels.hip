@@ -410,13 +410,50 @@ __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __r
                               int32_t* __restrict__ plane_slot, int64_t* __restrict__ accept_pos,
                               double* __restrict__ accept_psnr, int64_t accept_cap, int G, int P, int H, int W,
                               double count, int rel_scale, double peak) {
-  __shared__ int64_t s_pos;
-  __shared__ int s_done;
+  // One block.  Everything the serial decision reads is fetched into LDS first, by many lanes and
+  // under the partial reduction: the walk state, the K jobs, the base statistics, each candidate's
+  // mask word and the two slot pairs its commit would swap, and the order window the next batch
+  // starts in (pos + [0, 2K)).  The decision itself (one lane, in candidate order) then runs on
+  // LDS and registers; the r04j version issued its global loads one dependent round trip at a
+  // time inside that loop (11 us per launch, profiles/r04/walk_kernel_stats_r04j.txt).
   constexpr int CJ = 8;                     // jobs per staging round of the partials
   __shared__ double s_part[CJ * 3 * 128];   // RB <= 128 row blocks
   __shared__ double s_js[256 * 3];
+  __shared__ JobDesc s_job[256];
+  __shared__ uint64_t s_word[256];          // candidate c's mask word
+  __shared__ int32_t s_slot[256][4];        // plane_slot[pa], [pa + 1], [CH + 2c], [CH + 2c + 1]
+  __shared__ int64_t s_order[512];          // order[pos + i], i < 2K
+  __shared__ double s_base[3 * HBX_MAX_GROUPS];
+  __shared__ int64_t s_pos, s_total, s_acc;
+  __shared__ int s_done, s_stop_en;
+  __shared__ double s_prev, s_last, s_init, s_stop_diff;
   const int k = threadIdx.x;
   const int64_t hw = (int64_t)H * W;
+  const int CH = G * P;
+  if (k == 0) {
+    s_pos = w->pos; s_total = w->total; s_acc = w->accepted; s_done = w->done;
+    s_stop_en = w->stop_enabled; s_prev = w->prev_psnr; s_last = w->last_psnr;
+    s_init = w->init_psnr; s_stop_diff = w->stop_diff;
+  }
+  if (decide && k < K) {
+    const JobDesc jb = jobs[k];
+    s_job[k] = jb;
+    if (jb.env >= 0) {
+      const int ch = jb.group * P + jb.flip_plane;
+      s_word[k] = mask[(size_t)ch * H * (W / 64) + (size_t)(jb.flip_pix / W) * (W / 64) + (jb.flip_pix % W) / 64];
+      const int pa = jb.group * P + (jb.flip_plane & ~1);
+      s_slot[k][0] = plane_slot[pa];
+      s_slot[k][1] = plane_slot[pa + 1];
+      s_slot[k][2] = plane_slot[CH + 2 * k];
+      s_slot[k][3] = plane_slot[CH + 2 * k + 1];
+    }
+  }
+  if (decide && k < 3 * G) s_base[k] = base_stats[k];
+  __syncthreads();                          // s_pos
+  {
+    const int64_t p0 = s_pos;
+    for (int i = k; i < 2 * K; i += blockDim.x) s_order[i] = (p0 + i < s_total) ? order[p0 + i] : -1;
+  }
   if (decide) {
     // k_reduce_partials fused (one launch per batch less): each candidate's three statistics
     // summed over its row blocks in row-block order, k_reduce_partials' order bit for bit
@@ -433,74 +470,76 @@ __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __r
       __syncthreads();
     }
   }
-  const double* job_stats = s_js;
-  if (k == 0) {
-    s_pos = w->pos;
-    s_done = w->done;
-    if (decide && !s_done) {
-      const int64_t pos = s_pos;
-      const int nk = (int)min((int64_t)K, w->total - pos);
-      double prev = w->prev_psnr, last = w->last_psnr;
-      int64_t a = w->accepted;
-      unsigned touched = 0;
-      int visited = nk, done = 0;
-      for (int c = 0; c < nk; ++c) {
-        const JobDesc jb = jobs[c];
-        if (jb.env >= 0 && ((touched >> jb.group) & 1u)) { visited = c; break; }
-        double ps = NAN;
-        if (jb.env >= 0) {
-          const double* js = job_stats + 3 * (size_t)c;
-          double sxy = 0.0, sxx = 0.0, syy = 0.0;
-          for (int gg = 0; gg < G; ++gg) {    // k_eval_finalize's sum order
-            if (gg == jb.group) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
-            else { sxy += base_stats[3 * gg]; sxx += base_stats[3 * gg + 1]; syy += base_stats[3 * gg + 2]; }
-          }
-          ps = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
+  __syncthreads();
+  if (k == 0 && decide && !s_done) {
+    const int64_t pos = s_pos;
+    const int nk = (int)min((int64_t)K, s_total - pos);
+    double prev = s_prev, last = s_last;
+    int64_t a = s_acc;
+    unsigned touched = 0;
+    int visited = nk, done = 0;
+    for (int c = 0; c < nk; ++c) {
+      const JobDesc jb = s_job[c];
+      if (jb.env >= 0 && ((touched >> jb.group) & 1u)) { visited = c; break; }
+      double ps = NAN;
+      const double* js = s_js + 3 * c;
+      if (jb.env >= 0) {
+        double sxy = 0.0, sxx = 0.0, syy = 0.0;
+        for (int gg = 0; gg < G; ++gg) {    // k_eval_finalize's sum order
+          if (gg == jb.group) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
+          else { sxy += s_base[3 * gg]; sxx += s_base[3 * gg + 1]; syy += s_base[3 * gg + 2]; }
         }
-        last = ps;
-        if (ps > prev) {                     // commit candidate c
-          const int ch = jb.group * P + jb.flip_plane;
-          const int pix = jb.flip_pix;
-          mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64] ^=
-              (1ull << ((pix % W) & 63));
-          base_stats[3 * jb.group] = js_get(job_stats, c, 0);
-          base_stats[3 * jb.group + 1] = js_get(job_stats, c, 1);
-          base_stats[3 * jb.group + 2] = js_get(job_stats, c, 2);
-          const int CH = G * P, pa = jb.group * P + (jb.flip_plane & ~1);
-          for (int q = 0; q < 2; ++q) {
-            const int32_t cur = plane_slot[pa + q];
-            plane_slot[pa + q] = plane_slot[CH + 2 * c + q];
-            plane_slot[CH + 2 * c + q] = cur;
-          }
-          if (a < accept_cap) { accept_pos[a] = pos + c; accept_psnr[a] = ps; }
-          ++a;
-          prev = ps;
-          touched |= 1u << jb.group;
-          if (w->stop_enabled && ps - w->init_psnr >= w->stop_diff) {   // DBS_ratio_0.5.py:366-372
-            done = 1;
-            w->stopped_early = 1;
-            visited = c + 1;
-            break;
-          }
+        ps = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
+      }
+      last = ps;
+      if (ps > prev) {                     // commit candidate c
+        const int ch = jb.group * P + jb.flip_plane;
+        const int pix = jb.flip_pix;
+        mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64] =
+            s_word[c] ^ (1ull << ((pix % W) & 63));
+        s_base[3 * jb.group] = js[0];
+        s_base[3 * jb.group + 1] = js[1];
+        s_base[3 * jb.group + 2] = js[2];
+        base_stats[3 * jb.group] = js[0];
+        base_stats[3 * jb.group + 1] = js[1];
+        base_stats[3 * jb.group + 2] = js[2];
+        const int pa = jb.group * P + (jb.flip_plane & ~1);
+        plane_slot[pa] = s_slot[c][2];        // the fresh pair's slots become current,
+        plane_slot[pa + 1] = s_slot[c][3];
+        plane_slot[CH + 2 * c] = s_slot[c][0];    // the replaced ones become spares
+        plane_slot[CH + 2 * c + 1] = s_slot[c][1];
+        if (a < accept_cap) { accept_pos[a] = pos + c; accept_psnr[a] = ps; }
+        ++a;
+        prev = ps;
+        touched |= 1u << jb.group;
+        if (s_stop_en && ps - s_init >= s_stop_diff) {   // DBS_ratio_0.5.py:366-372
+          done = 1;
+          w->stopped_early = 1;
+          visited = c + 1;
+          break;
         }
       }
-      w->accepted = a;
-      w->prev_psnr = prev;
-      w->last_psnr = last;
-      w->pos = pos + visited;
-      w->batches += 1;
-      if (done || w->pos >= w->total) w->done = 1;
-      s_pos = w->pos;
-      s_done = w->done;
     }
+    w->accepted = a;
+    w->prev_psnr = prev;
+    w->last_psnr = last;
+    w->pos = pos + visited;
+    w->batches += 1;
+    const int d = (done || pos + visited >= s_total) ? 1 : 0;
+    if (d) w->done = 1;
+    s_done = d;
+    s_acc = visited;                         // reused: the next batch's offset in the order window
+  } else if (k == 0) {
+    s_acc = 0;
   }
   __syncthreads();
   if (k < K) {                            // the next batch's jobs
-    const int64_t q = s_pos + k;
+    const int off = (int)s_acc;
+    const int64_t q = s_pos + off + k;
     JobDesc jd;
     jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
-    if (!s_done && q < w->total) {
-      const int64_t av = order[q];
+    if (!s_done && q < s_total) {
+      const int64_t av = s_order[off + k];
       if (av >= 0 && av < (int64_t)G * P * hw) {
         const int ch = (int)(av / hw);
         jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(av % hw);
