@@ -414,8 +414,10 @@ __global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __r
   // under the partial reduction: the walk state, the K jobs, the base statistics, each candidate's
   // mask word and the two slot pairs its commit would swap, and the order window the next batch
   // starts in (pos + [0, 2K)).  The decision itself (one lane, in candidate order) then runs on
-  // LDS and registers; the r04j version issued its global loads one dependent round trip at a
-  // time inside that loop (11 us per launch, profiles/r04/walk_kernel_stats_r04j.txt).
+  // LDS and registers.  Measured: 11.7 us per launch against 11.0 for the r04j version that
+  // issued its global loads inside the loop (profiles/r04/walk_kernel_stats_r04{j,k}.txt) -- the
+  // launch is bound by its fixed chain (state -> order window / partials -> reduction ->
+  // decision -> job writes), not by the loop's loads.
   constexpr int CJ = 8;                     // jobs per staging round of the partials
   __shared__ double s_part[CJ * 3 * 128];   // RB <= 128 row blocks
   __shared__ double s_js[256 * 3];
