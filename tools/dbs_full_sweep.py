@@ -1,9 +1,11 @@
 """BASELINE configs[1] end to end: DBS_1024_24.py's greedy pixel-flip sweep over ALL
 24 x 1024 x 1024 = 25,165,824 candidates of one image (synthetic seeded pre-model /
-target, order = rng(3).permutation), on the device-resident walk
-(hbx.dbs.greedy mode="psf", exact refresh every 4096 accepts).  Prints a progress
-line every ~20 s and one JSON summary line at the end.
-python tools/dbs_full_sweep.py [n_candidates]"""
+target, order = rng(3).permutation), on the device-resident walk: mode "psf" (the
+incremental-field walk, hbx.dbs.greedy mode="psf", exact refresh every 4096 accepts) or "fft"
+(the reference's algorithm -- every candidate an f32 re-propagation, on the plane cache with
+device-decided batches, hbx_dbs_walk_planes).  Prints a progress line every ~20 s and one JSON
+summary line at the end.
+python tools/dbs_full_sweep.py [n_candidates] [psf|fft]"""
 import json
 import os
 import sys
@@ -19,7 +21,9 @@ import hbx  # noqa: E402
 from hbx import dbs  # noqa: E402
 
 total = 24 * 1024 * 1024
-n = int(sys.argv[1]) if len(sys.argv) > 1 else total
+n = int(sys.argv[1]) if len(sys.argv) > 1 and int(sys.argv[1]) > 0 else total
+mode = sys.argv[2] if len(sys.argv) > 2 else "psf"
+assert mode in ("psf", "fft")
 cfg = hbx.rgb_config(1024)
 g = torch.Generator(device="cuda").manual_seed(0)
 pre = torch.rand((24, 1024, 1024), generator=g, device="cuda")
@@ -27,7 +31,7 @@ tgt = torch.rand((3, 1024, 1024), generator=g, device="cuda")
 order = np.random.default_rng(3).permutation(total)[:n]
 plan = hbx.Plan(cfg, max_jobs=64)
 mask = hbx.pack_bits(pre >= 0.5)
-dbs.greedy(plan, mask.clone(), tgt, order[:4096], mode="psf")   # warm-up
+dbs.greedy(plan, mask.clone(), tgt, order[:4096], mode=mode)   # warm-up
 torch.cuda.synchronize()
 last = [0.0]
 
@@ -40,7 +44,7 @@ def progress(pos, acc, psnr, sec):
 
 
 t0 = time.perf_counter()
-res = dbs.greedy(plan, mask, tgt, order, mode="psf", progress=progress)
+res = dbs.greedy(plan, mask, tgt, order, mode=mode, progress=progress)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 _, _, ps = plan.propagate(mask[None], tgt[None], want_intensity=False)
@@ -51,5 +55,7 @@ print(json.dumps({
     "candidates_per_s": round(res.steps / dt, 1), "batches": res.launches,
     "initial_psnr": res.initial_psnr, "final_psnr": res.final_psnr, "final_psnr_exact_repropagation": exact,
     "final_psnr_drift_db": abs(exact - res.final_psnr),
-    "mode": "device-resident walk (hbx_dbs_walk_psf), exact refresh every 4096 accepts",
+    "mode": ("device-resident walk (hbx_dbs_walk_psf), exact refresh every 4096 accepts" if mode == "psf" else
+             "FFT mode (f32 re-propagation per candidate, the reference's algorithm) on the plane cache, "
+             "device-decided batches (hbx_dbs_walk_planes)"),
     "data": "synthetic seeded U[0,1) pre-model (threshold 0.5) and target"}))
