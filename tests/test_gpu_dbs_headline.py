@@ -215,6 +215,47 @@ def test_fft_greedy_plane_cache_equals_full_repropagation(golden_dir, name, stop
     assert len(full.accepted_positions) > 100
 
 
+def test_fft_walk_edge_orders(golden_dir):
+    """The device-decided FFT-mode walk (hbx_dbs_walk_planes) on the orders that stress its batch
+    logic, each against the host-decided full re-propagation (planes=False): an empty order, one
+    candidate, fewer candidates than K, every position repeated (an accepted pixel comes back in
+    the same batch: its group is touched, the batch must end there), runs of one colour group
+    (at most one accept per batch), k_max 1 and 7, and an early stop.  Same accepts,
+    same PSNR bits, same final mask."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
+    hw = 1024 * 1024
+    base = [int(v) for v in order[:600]]
+    same_group = [int(v) for v in order[:4000] if int(v) // (8 * hw) == 1][:200]
+    cases = {
+        "empty": ([], {}),
+        "one": (base[:1], {}),
+        "short": (base[:3], {"k_max": 8}),
+        "repeated": ([v for v in base[:150] for _ in range(2)], {}),
+        "one_group": (same_group, {}),
+        "kmax1": (base[:300], {"k_max": 1}),
+        "kmax7": (base[:300], {"k_max": 7}),
+        "stop": (base, {"stop_diff": 1e-4}),
+    }
+    for name, (o, kw) in cases.items():
+        o = np.asarray(o, np.int64)
+        runs = []
+        for planes, walk in ((False, False), (True, True)):
+            plan, mask, target = _dev(ocfg, pre, tgt)
+            res = dbs.greedy(plan, mask, target, o, mode="fft", planes=planes, device_walk=walk, **kw)
+            runs.append((res, mask.cpu().numpy()))
+            plan.close()
+        (full, m_full), (walk, m_walk) = runs
+        assert walk.accepted_positions == full.accepted_positions, name
+        assert walk.accepted_psnr == full.accepted_psnr, name
+        assert walk.steps == full.steps and walk.stopped_early == full.stopped_early, name
+        assert np.array_equal(m_full, m_walk), name
+        if name == "repeated":
+            assert len(walk.accepted_positions) > 10
+        if name == "stop":
+            assert walk.stopped_early and walk.steps < len(o)
+
+
 def test_candidate_change_precision_1024x24(golden_dir):
     """Each candidate's PSNR change against the initial state, accepted or not
     (probe sweep / speculative batches): incremental path within INCR_TOL_DB,
