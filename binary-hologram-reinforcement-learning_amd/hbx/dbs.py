@@ -556,6 +556,12 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     if mode not in ("fft", "psf", "psf_host"):
         raise ValueError(f"mode must be 'fft', 'psf' or 'psf_host', got {mode!r}")
     dev = plan.device
+    if len(order) == 0 or max_candidates == 0:
+        # nothing to visit: the serial loop's result over zero candidates (the device walks take
+        # a non-empty order)
+        _, _, p0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False, stream=stream)
+        init = float(p0.item())
+        return GreedyResult(init, init, 0, [], [], 0)
     if mode == "psf":
         order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
         total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
