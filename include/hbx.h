@@ -220,7 +220,9 @@ int hbx_env_reset(hbx_plan_t plan, const hbx_env_buffers_t* env, int32_t n_env,
  * per-flip RGB with cached other-group statistics).  One action per env:
  * decode (env.py:157-161), flip + record, re-propagate the touched colour
  * group, relative PSNR, reward = RW * delta, rollback / bonus / termination.
- *   reward, psnr [B] f64; accepted, terminated, truncated [B] u8 (nullable)
+ *   reward, psnr [B] f64; accepted, terminated, truncated [B] u8 (nullable; device
+ *   addresses, e.g. of hbx_host_alloc'd host-mapped memory -- ABI v11: the kernels then
+ *   write the results straight to the host, readable once the stream work is done)
  *   group_intensity [B][H][W] f32: the stepped (pre-rollback) group mean
  *   (nullable; not together with env->recon, which already holds it).
  * With env->recon (ABI v8) the last pass writes the stepped intensity straight
