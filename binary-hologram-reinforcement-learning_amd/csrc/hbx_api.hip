@@ -105,7 +105,8 @@ int hbx_host_alloc(size_t bytes, void** host, void** device) {
   *host = nullptr;
   *device = nullptr;
   void* h = nullptr;
-  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !h)
+  // portable: a rank's process may run on any device (LOCAL_RANK), not the current one at alloc
+  if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess || !h)
     return fail(HBX_ERR_NOMEM, "hipHostMalloc");
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
