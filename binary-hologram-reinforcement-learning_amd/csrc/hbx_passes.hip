@@ -637,9 +637,7 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
 // plane's FFT is done (two blocks per CU cover them; a second register set for a plane in
 // flight took one block per CU and measured 1.80 ms against 1.47).  The r02
 // kernel staged every plane through an LDS tile between three block barriers (1.80 ms).
-// STEP: the plane-cached step's variant (kPlanesStep only: the pair + the cached planes), compiled
-// apart so the full pass keeps its own register budget (N = 256: 116 VGPRs, 4 waves / SIMD)
-template <int R, bool STEP = false>
+template <int R>
 __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__ jobs,
                                                      const float2* __restrict__ ws_b,
                                                      const float* __restrict__ target,
@@ -726,48 +724,26 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
   };
   // a cached plane's |U_q|^2 added in its place in the plane order (the sum is the FFT mode's
   // sum bit for bit: acc = ((0 + c_0) + c_1) + ..., each c_q the same f32 value)
-  auto issue_cached = [&](float (&c)[R], int q) {
+  auto add_cached = [&](int q) {
     const float* crow = pool_row(slots[jb.group * P + q]);
+    float c[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) c[k] = __builtin_nontemporal_load(crow + t + R * k);
-  };
-  auto add_cached = [&](const float (&c)[R]) {
 #pragma unroll
     for (int k = 0; k < R; ++k) acc[k] += c[k];
   };
   pk2 va[R];
-  if constexpr (STEP) {   // only the flipped plane's pair is in B
-    // The P - 2 cached planes go through two register rows, each issued one plane ahead of its
-    // add (r04: the r03 loop issued a plane's loads only after the previous plane's adds, one
-    // memory round trip per cached plane -- k_rowinv_d ran at 0.35 of 8 TB/s in the plane-cached
-    // step, profiles/r04/bench_r04j.json); the pair's B rows fly under the first cached adds.
-    // pa and P are even, so both runs of cached planes (before and after the pair) pair up.
+  if (plane_mode == kPlanesStep) {   // only the flipped plane's pair is in B
     const int pa = jb.flip_plane & ~1;
-    float c0[R], c1[R];
     load_plane(va, pa);
-    {
-      const int first = pa > 0 ? 0 : 2;
-      if (first < P) issue_cached(c0, first);
-    }
     __syncthreads();  // tw visible
 #pragma unroll 1
-    for (int q = 0; q < pa; q += 2) {
-      issue_cached(c1, q + 1);
-      add_cached(c0);
-      const int nx = q + 2 < pa ? q + 2 : pa + 2;
-      if (nx < P) issue_cached(c0, nx);
-      add_cached(c1);
-    }
+    for (int q = 0; q < pa; ++q) add_cached(q);
     finish_plane(va, pa);
     load_plane(va, pa + 1);
     finish_plane(va, pa + 1);
 #pragma unroll 1
-    for (int q = pa + 2; q < P; q += 2) {
-      issue_cached(c1, q + 1);
-      add_cached(c0);
-      if (q + 2 < P) issue_cached(c0, q + 2);
-      add_cached(c1);
-    }
+    for (int q = pa + 2; q < P; ++q) add_cached(q);
     rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red,
                            rc_pending, rc_cache);
     return;
@@ -1078,22 +1054,15 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
-    if constexpr (kTiledB<R>) {
-      if (pd.plane_mode == kPlanesStep)
-        hipLaunchKernelGGL((k_rowinv_d<R, true>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
+    if constexpr (kTiledB<R>)
+      hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
                          pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
                          pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot, pd.plane_spares,
                          pd.spare_base, pd.rc_pending, pd.rc_cache);
-      else
-        hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
-                         pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
-                         pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot, pd.plane_spares,
-                         pd.spare_base, pd.rc_pending, pd.rc_cache);
-    } else {
+    else
       hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                          target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,
                          field_out, target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
-    }
     if (tm) tm->end(2, n_jobs, st);
   }
   if (!pd.skip_reduce)
