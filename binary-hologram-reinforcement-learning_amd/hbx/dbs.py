@@ -500,14 +500,18 @@ def _walk_stream(device, i: int):
 def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: Sequence[torch.Tensor], orders,
                 stop_diff: Optional[float] = None, k_max: Optional[int] = None,
                 max_candidates: Optional[int] = None, refresh_every: int = 4096,
-                concurrency: int = 4) -> List[GreedyResult]:
+                concurrency: int = 4, mode: str = "psf") -> List[GreedyResult]:
     """DBS_1024_24.py's loop over several images (`:208-211`), up to `concurrency`
     images' greedy walks side by side: walk i on plans[i] (one plan per image:
     its own workspace, tables and walk buffers) and its own HIP stream, the host
     advancing the walks in turn, so their latency-bound launches overlap on the
     GPU (1024x24: 188k candidates/s over 4 walks against 97k for one, r02; 8
-    walks 191k).  Each walk's result is
-    exactly greedy(mode="psf") on that image alone; masks are modified in place."""
+    walks 191k).  mode "psf": the incremental-field walks (each result exactly
+    greedy(mode="psf") on that image alone); "fft": the FFT-mode walks on the plane cache
+    (hbx_dbs_walk_planes; each result exactly greedy(mode="fft") on that image alone).
+    Masks are modified in place."""
+    if mode not in ("psf", "fft"):
+        raise ValueError(f"greedy_many: mode must be 'psf' or 'fft', got {mode!r}")
     if not (len(plans) == len(masks) == len(targets) == len(orders)):
         raise ValueError("one plan, mask, target and order per image")
     step = max(1, int(concurrency))
@@ -522,13 +526,21 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
                                              orders[g0:g0 + step]):
             order_t = torch.as_tensor(np.asarray(order, np.int64)).to(plan.device)
             total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
-            walks.append(_Walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
-                               _walk_stream(plan.device, len(walks)), refresh_every))
-        while not all(w.finished for w in walks):
-            for w in walks:
+            if total == 0:                     # nothing to visit (the device walks take a non-empty order)
+                walks.append(greedy(plan, mask, target, [], mode="fft" if mode == "fft" else "psf"))
+            elif mode == "fft":
+                km = min(k_max or plan.max_jobs, plan.max_jobs)
+                walks.append(_PlanesWalk(plan, mask, target, order_t, total, stop_diff, 1, km,
+                                         _walk_stream(plan.device, len(walks)), 0))
+            else:
+                walks.append(_Walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
+                                   _walk_stream(plan.device, len(walks)), refresh_every))
+        live = [w for w in walks if not isinstance(w, GreedyResult)]
+        while not all(w.finished for w in live):
+            for w in live:
                 w.advance()
         torch.cuda.synchronize()
-        results.extend(w.result() for w in walks)
+        results.extend(w if isinstance(w, GreedyResult) else w.result() for w in walks)
     return results
 
 

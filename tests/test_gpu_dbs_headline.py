@@ -256,6 +256,36 @@ def test_fft_walk_edge_orders(golden_dir):
             assert walk.stopped_early and walk.steps < len(o)
 
 
+def test_fft_greedy_many_equals_single_walks(golden_dir):
+    """dbs.greedy_many(mode="fft"): several images' FFT-mode walks side by side (one plan and
+    stream each) give every image exactly its greedy(mode="fft") result -- accepts, PSNR bits,
+    final mask -- including an empty order and an early stop."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
+    rng = np.random.default_rng(5)
+    imgs = [(pre, tgt, order[:2500])]
+    for i in range(2):
+        imgs.append((rng.random(pre.shape).astype(pre.dtype), rng.random(tgt.shape).astype(tgt.dtype),
+                     rng.permutation(order)[:2000 + 300 * i]))
+    imgs.append((pre, tgt, order[:0]))
+    for stop in (None, 2e-4):
+        single = []
+        for p_, t_, o_ in imgs:
+            plan, mask, target = _dev(ocfg, p_, t_, max_jobs=16)
+            single.append((dbs.greedy(plan, mask, target, o_, mode="fft", stop_diff=stop), mask.cpu().numpy()))
+            plan.close()
+        devs = [_dev(ocfg, p_, t_, max_jobs=16) for p_, t_, _ in imgs]
+        many = dbs.greedy_many([x[0] for x in devs], [x[1] for x in devs], [x[2] for x in devs],
+                               [o_ for _, _, o_ in imgs], stop_diff=stop, mode="fft")
+        for (want, wm), got, (plan, gm, _) in zip(single, many, devs):
+            assert got.accepted_positions == want.accepted_positions, stop
+            assert got.accepted_psnr == want.accepted_psnr, stop
+            assert got.steps == want.steps and got.stopped_early == want.stopped_early, stop
+            assert np.array_equal(gm.cpu().numpy(), wm), stop
+            plan.close()
+        assert sum(len(r.accepted_positions) for r in many) > 100
+
+
 def test_candidate_change_precision_1024x24(golden_dir):
     """Each candidate's PSNR change against the initial state, accepted or not
     (probe sweep / speculative batches): incremental path within INCR_TOL_DB,
