@@ -220,6 +220,26 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     torch.cuda.synchronize()
     dtf = time.perf_counter() - t0
     kpos = [p for p in res.accepted_positions if p < nf]
+    # several images side by side in FFT mode (DBS_1024_24.py loops over a folder, :208-211)
+    n_img, n_each = 4, min(n_flips, 16384)
+    fplans = [Plan(cfg, max_jobs=16) for _ in range(n_img)]
+    fgens = [torch.Generator(device=mask.device).manual_seed(200 + i) for i in range(n_img)]
+    fmasks = [hbx_pack(torch.rand((CH, N, N), generator=gg, device=mask.device) >= 0.5) for gg in fgens]
+    ftgts = [torch.rand((cfg.groups, N, N), generator=gg, device=mask.device) for gg in fgens]
+    forders = [np.random.default_rng(30 + i).permutation(CH * N * N)[:n_each] for i in range(n_img)]
+    dbs.greedy_many(fplans, [m.clone() for m in fmasks], ftgts, [o[:256] for o in forders], mode="fft")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    fres = dbs.greedy_many(fplans, fmasks, ftgts, forders, mode="fft")
+    torch.cuda.synchronize()
+    dtf4 = time.perf_counter() - t0
+    for pl in fplans:
+        pl.close()
+    out["several_images"] = {"images": n_img, "flips": sum(r.steps for r in fres), "seconds": round(dtf4, 3),
+                             "flips_per_s_aggregate": round(sum(r.steps for r in fres) / dtf4, 1),
+                             "accepted": sum(len(r.accepted_positions) for r in fres),
+                             "note": "hbx.dbs.greedy_many(mode='fft'): one FFT-mode walk per image (own plan, "
+                                     "plane cache and HIP stream), synthetic seeded images"}
     out["full_repropagation"] = {
         "flips": rf.steps, "seconds": round(dtf, 3), "flips_per_s": round(rf.steps / dtf, 1),
         "same_accepts_and_psnr_bits_as_plane_cache": bool(
