@@ -705,6 +705,10 @@ class HologramVecEnv(_VecEnvBase):
     def close(self):
         if self._readback is not None:
             self._readback.synchronize()
+        # every view of the host-mapped row goes before the memory does
+        self._host_t = self._host_np = self._h_rew = self._h_term = self._h_trunc = self._h_err = None
+        self._fast_args = None
+        self._graph = None
         self._hrow.close()
         self.plan.close()
 
