@@ -329,3 +329,31 @@ def test_step_settles_accepted_groups():
     assert n_acc > 0 and n_rej > 0
     env.close()
     twin.close()
+
+
+def test_step_chunked_batches_equal_one_batch():
+    """A VecEnv whose plan holds fewer jobs than envs (max_jobs 4, 10 envs: three chunks per step,
+    each decoding its actions in the first pass and reducing in its finalize) steps exactly like
+    the one-chunk env: rewards, PSNRs, accept flags, observations; an out-of-range action in the
+    last chunk raises through the mirrored error word."""
+    import hbx
+    cfg = hbx.mono_config(256)
+    B = 10
+    a, g = _env(cfg, B, 41, max_jobs=4)
+    b, _ = _env(cfg, B, 41)
+    oa, ob = a.reset(), b.reset()
+    assert torch.equal(oa["recon_image"], ob["recon_image"])
+    acts = torch.randint(0, cfg.channels * 256 * 256, (60, B), generator=g, device="cuda")
+    for k in range(60):
+        oa, ra, da, _ = a.step(acts[k])
+        ob, rb, db, _ = b.step(acts[k])
+        la, lb = a.last_step(), b.last_step()
+        assert np.array_equal(ra, rb) and np.array_equal(da, db), k
+        assert np.array_equal(la["psnr"], lb["psnr"]) and np.array_equal(la["accepted"], lb["accepted"]), k
+        assert torch.equal(oa["recon_image"], ob["recon_image"]) and torch.equal(oa["state"], ob["state"]), k
+    bad = acts[0].clone()
+    bad[9] = -5
+    with pytest.raises(ValueError):
+        a.step(bad)
+    a.close()
+    b.close()
