@@ -42,8 +42,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--envs", type=int, default=128, help="envs per GPU")
     ap.add_argument("--size", type=int, default=1024)
-    ap.add_argument("--cpu-sample", type=int, default=12,
-                    help="env-steps of the numpy oracle timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=20,
+                    help="env-steps of the numpy oracle timed for cpu_baseline, after 2 warm-ups "
+                         "(SURVEY 8d: >= 20; 0 = skip)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in single-env lines (dropin_env_256 / dropin_env_1024x24)")
     ap.add_argument("--no-psnr-check", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-pg", action="store_true",
@@ -146,6 +149,27 @@ def canonical_step_bytes(N: int, P: int) -> int:
     return P * 4 * (8 * N * N) + 4 * N * N + P * N * N // 8
 
 
+def cpu_model() -> str:
+    """The host CPU's model string (/proc/cpuinfo "model name", what lscpu prints)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def host_cpus() -> int:
+    """CPUs this process may run on (the box's share, not the whole machine)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline_scipy(n_steps: int, N: int, workers: int):
     """SURVEY 8d's second CPU figure: the same env-step with scipy.fft complex64
     over `workers` threads (numpy oracle for everything but the transforms)."""
@@ -174,7 +198,8 @@ def cpu_baseline_scipy(n_steps: int, N: int, workers: int):
         step(a)
     dt = time.perf_counter() - t0
     return {"value": n_steps / dt, "unit": "env-steps/s", "cores": workers, "kind": "port",
-            "sample": f"{n_steps} env-steps, scipy.fft complex64 with workers={workers}, {dt:.1f} s"}
+            "cpu_model": cpu_model(), "host_cpus_visible": host_cpus(), "steps": n_steps, "warmup": 2,
+            "sample": f"{n_steps} env-steps after 2 warm-ups, scipy.fft complex64 with workers={workers}, {dt:.1f} s"}
 
 
 def dbs_prefix(cfg, mask, target, n_flips: int):
@@ -427,7 +452,8 @@ def cpu_baseline(n_steps: int, N: int):
         env.step(int(a))
     dt = time.perf_counter() - t0
     return {"value": n_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_steps} env-steps of the {N}x{N}x24 RGB env (one 8-plane group propagate each), "
+            "cpu_model": cpu_model(), "host_cpus_visible": host_cpus(), "steps": n_steps, "warmup": 2,
+            "sample": f"{n_steps} env-steps after 2 warm-ups of the {N}x{N}x24 RGB env (one 8-plane group propagate each), "
                       f"numpy.fft complex128 oracle (oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
 
 
@@ -448,11 +474,12 @@ def cpu_baseline_mono(n_steps: int, N: int = 256):
         env.step(int(a))
     dt = time.perf_counter() - t0
     return {"value": n_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_steps} env-steps of the {N}x{N}x8 mono env (env.py), numpy.fft complex128 oracle "
+            "cpu_model": cpu_model(), "host_cpus_visible": host_cpus(), "steps": n_steps, "warmup": 2,
+            "sample": f"{n_steps} env-steps after 2 warm-ups of the {N}x{N}x8 mono env (env.py), numpy.fft complex128 oracle "
                       f"(oracle/hbx_oracle.py), 1 thread, {dt:.1f} s"}
 
 
-def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=False, reps=3):
+def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=False, reps=3, obs_format="torch"):
     """The step an SB3 learner calls (train-PPO.py:296-322): HologramVecEnv.step with all
     five observation keys (env.py:176-181) as device tensors, rewards / dones to the host,
     every step.  The observations are views of buffers the step kernels keep current
@@ -463,7 +490,7 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
     import statistics
     import torch
     from hbx.env import OBS_KEYS, HologramVecEnv
-    vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format="torch",
+    vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format=obs_format,
                          auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9, refresh_every=0,
                          graph=graph)
     pure = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=(), auto_reset=False,
@@ -492,17 +519,18 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
     dt = statistics.median(t_obs)
     pure_ms = statistics.median(t_pure) / steps * 1e3
     pure.close()
-    shapes = {k: list(v.shape) for k, v in obs.items()}
+    dev_obs = {k: obs.device(k) for k in obs.keys()} if obs_format == "lazy" else obs
+    shapes = {k: list(v.shape) for k, v in dev_obs.items()}
     views = all(v.data_ptr() == getattr(vec.state, a).data_ptr() for k, v, a in
-                ((k, obs[k], {"state_record": "record", "state": "state_bytes", "pre_model": "pre_model",
-                              "recon_image": "recon", "target_image": "target"}[k]) for k in obs))
+                ((k, dev_obs[k], {"state_record": "record", "state": "state_bytes", "pre_model": "pre_model",
+                                  "recon_image": "recon", "target_image": "target"}[k]) for k in dev_obs))
     vec.close()
     ms = dt / steps * 1e3
     return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps, "reps": reps,
             "graph": graph, "ms_per_step": round(ms, 4), "bare_step_ms": round(bare_ms, 4),
             "obs_overhead_frac": round(ms / bare_ms - 1.0, 4),
             "pure_device_step_ms": round(pure_ms, 4), "overhead_vs_pure_device_step": round(ms / pure_ms - 1.0, 4),
-            "obs_keys": list(obs.keys()), "obs_shapes": shapes, "obs_are_views": views,
+            "obs_format": obs_format, "obs_keys": list(obs.keys()), "obs_shapes": shapes, "obs_are_views": views,
             "note": "HologramVecEnv.step (SB3 VecEnv surface, obs_format='torch', auto_reset on): all five "
                     "observation keys returned as views of device buffers the step kernels keep current "
                     "(state as int8, stepped pre-rollback recon_image), rewards / dones / error word written "
@@ -510,6 +538,211 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
                     "ppo_mono_256 line's device step (same measurement as the headline: sampled pass timing "
                     "and the per-8-step metric gather included); pure_device_step_ms is step_device of a twin "
                     "env without observations, timing or gather, alternated with the VecEnv runs"}
+
+
+def dropin_env(N: int, G: int, steps: int, warmup: int):
+    """configs[0] on the GPU: the drop-in single env hbx.env.BinaryHologramEnv (B = 1) -- the
+    object train-PPO.py's DummyVecEnv(n_envs=1) steps (train-PPO.py:40,275-313) -- with the
+    reference's numpy observation dict every step (env.py:154-259).  Synthetic seeded image
+    (SURVEY 8d seeds 0 / 1 / 2); thresholds out of reach so no episode ends in the timed loop."""
+    import numpy as np
+    import torch
+    from hbx.env import BinaryHologramEnv
+    from hbx.plan import mono_config, rgb_config
+    cfg = mono_config(N) if G == 1 else rgb_config(N)
+    CH = cfg.channels
+    pre = np.random.default_rng(0).random((CH, N, N), np.float32)
+    tgt = np.random.default_rng(1).random((G, N, N), np.float32)
+    loader = [(torch.from_numpy(tgt[None]), ["synthetic.png"])]
+    env = BinaryHologramEnv(lambda t: torch.from_numpy(pre[None]).to(t.device), loader, max_steps=10 ** 9,
+                            T_PSNR=1e9, T_PSNR_DIFF=1e9, config=cfg, verbose=False)
+    env.reset()
+    acts = np.random.default_rng(2).integers(0, CH * N * N, warmup + steps).tolist()
+    for a in acts[:warmup]:
+        env.step(a)
+    s0 = env.host_syncs
+    t0 = time.perf_counter()
+    for a in acts[warmup:]:
+        obs, reward, term, trunc, info = env.step(a)
+    dt = time.perf_counter() - t0
+    syncs = (env.host_syncs - s0) / steps
+    env.close()
+    return {"value": round(steps / dt, 2), "unit": "env-steps/s", "envs": 1, "steps": steps,
+            "ms_per_step": round(dt / steps * 1e3, 4), "host_syncs_per_step": syncs,
+            "obs": {k: [list(v.shape), str(v.dtype)] for k, v in obs.items()},
+            "note": "hbx.env.BinaryHologramEnv.step (gymnasium contract, numpy obs dict): action into "
+                    "host-mapped memory, the device step, the recon D2H behind it, one wait; "
+                    "state / state_record / pre_model / target are host mirrors (env.py:176-181)"}
+
+
+def torch_reference_step(N: int, steps: int, warmup: int):
+    """What the reference's env.step costs on THIS GPU with PyTorch-ROCm doing its physics:
+    env.py:164-188 restated with torch ops (full int8 -> f32 mask H2D per step, torch.fft
+    fft2 / x H / ifft2 of the 8 planes, |.|^2, plane mean, least-squares relative PSNR, the
+    .item() sync of the comparison).  Not our path: a baseline for the drop-in env at B = 1
+    (torchOptics itself is absent; this assumes it is torch.fft-based)."""
+    import numpy as np
+    import torch
+    from hbx.plan import mono_config
+    cfg = mono_config(N)
+    P = cfg.planes
+    fx = np.fft.fftfreq(N, cfg.dx)
+    fy = np.fft.fftfreq(N, cfg.dy)
+    arg = 1.0 / cfg.wavelengths[0] ** 2 - fx[None, :] ** 2 - fy[:, None] ** 2
+    H = torch.from_numpy(np.exp(2j * np.pi * cfg.z * np.sqrt(np.maximum(arg, 0))).astype(np.complex64)).cuda()
+    state = (np.random.default_rng(0).random((1, P, N, N), np.float32) >= 0.5).astype(np.int8)
+    target = torch.from_numpy(np.random.default_rng(1).random((1, 1, N, N), np.float32)).cuda()
+    acts = np.random.default_rng(2).integers(0, P * N * N, warmup + steps)
+
+    def psnr_of(st):
+        u = torch.tensor(st, dtype=torch.float32).cuda()
+        f = torch.fft.ifft2(torch.fft.fft2(u) * H)
+        res = torch.mean(f.abs() ** 2, dim=1, keepdim=True)
+        x, y = res.double(), target.double()
+        s = torch.sum(x * y) / torch.sum(x * x)
+        mse = torch.mean((s * x - y) ** 2)
+        return float((10 * torch.log10(1.0 / mse)).item())
+
+    prev = psnr_of(state)
+
+    def step(a):
+        nonlocal prev
+        c, k = divmod(int(a), N * N)
+        r, col = divmod(k, N)
+        state[0, c, r, col] ^= 1
+        p = psnr_of(state)
+        if p - prev < 0:
+            state[0, c, r, col] ^= 1
+        else:
+            prev = p
+
+    for a in acts[:warmup]:
+        step(a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a in acts[warmup:]:
+        step(a)
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 2), "unit": "env-steps/s", "steps": steps,
+            "ms_per_step": round(dt / steps * 1e3, 4),
+            "note": "env.py:164-196's step with torch.fft (hipFFT) on this GPU, B = 1: the reference's "
+                    "algorithm as PyTorch would run it, for scale -- not the product path"}
+
+
+def shim_dbs_loop(N: int, flips: int, warmup: int):
+    """An unchanged DBS.py-style caller (DBS.py:247-294) driving the torchOptics shim: per flip,
+    the numpy state flipped, torch.tensor(state).cuda(), tt.Tensor(meta), tt.simulate(., z).abs()**2,
+    the plane mean, tt.relativeLoss(., target, tm.get_PSNR), strict accept or undo.  Builder-written
+    against the contract, timed on env.py's 256x256x8 mono."""
+    import numpy as np
+    import torch
+    import torchOptics.metrics as tm
+    import torchOptics.optics as tt
+    from hbx.plan import PIXEL_PITCH
+    P = 8
+    state = (np.random.default_rng(0).random((1, P, N, N), np.float32) >= 0.5).astype(np.int8)
+    target = torch.from_numpy(np.random.default_rng(1).random((1, 1, N, N), np.float32)).cuda()
+    order = np.random.default_rng(3).permutation(P * N * N)[:warmup + flips]
+    meta = {"dx": (PIXEL_PITCH, PIXEL_PITCH), "wl": 515e-9}
+
+    def psnr_of():
+        x = tt.Tensor(torch.tensor(state, dtype=torch.float32).cuda(), meta=meta)
+        res = torch.mean(tt.simulate(x, 2e-3).abs() ** 2, dim=1, keepdim=True)
+        return tt.relativeLoss(res, target, tm.get_PSNR)
+
+    prev = psnr_of()
+    acc = 0
+
+    def flip(a):
+        nonlocal prev, acc
+        c, k = divmod(int(a), N * N)
+        r, col = divmod(k, N)
+        state[0, c, r, col] = 1 - state[0, c, r, col]
+        p = psnr_of()
+        if p > prev:
+            prev, acc = p, acc + 1
+        else:
+            state[0, c, r, col] = 1 - state[0, c, r, col]
+
+    for a in order[:warmup]:
+        flip(a)
+    torch.cuda.synchronize()
+    a0 = acc
+    t0 = time.perf_counter()
+    for a in order[warmup:]:
+        flip(a)
+    dt = time.perf_counter() - t0
+    return {"value": round(flips / dt, 2), "unit": "candidates/s", "flips": flips, "accepted": acc - a0,
+            "ms_per_flip": round(dt / flips * 1e3, 4),
+            "note": "DBS.py:247-294's per-flip loop shape through torchOptics.optics.simulate / relativeLoss "
+                    "(hbx_simulate underneath): full mask H2D, 8-plane propagation returning complex fields, "
+                    "a host PSNR per flip -- the unchanged-caller path, not the device walk (dbs_greedy)"}
+
+
+def check_devices(rows, world: int, rehearse: bool, dev) -> int:
+    """The number of distinct GPUs the ranks ran on (rank 0's view of hbx.dist.describe_devices
+    rows, agreed by every rank).  Outside a rehearsal a line whose ranks did not run on `world`
+    distinct GPUs is refused: every rank exits non-zero (SystemExit), so no number is printed
+    for a world that time-shared devices."""
+    from hbx import dist as hd
+    n = hd.distinct_devices(rows) if rows else 0
+    bad = 0.0 if (rehearse or n == world) else 1.0
+    if hd.max_over_ranks(bad if rows else 0.0, dev) > 0:
+        raise SystemExit(f"bench.py: {world} ranks ran on {n} distinct GPU(s) ({rows}); "
+                         "a multi-GPU line needs one GPU per rank (HBX_BENCH_REHEARSE_ONE_GPU=1 rehearses)")
+    return n
+
+
+def vecenv_step_sharded(mcfg, B, steps, warmup, tsrc, psrc, every, dev, world):
+    """world > 1 (BASELINE configs[3], train-PPO.py:275-322 at 128 envs per GPU): every rank's
+    SB3-facing step (HologramVecEnv.step, all five observations, numpy rewards / dones on the
+    host) with the rewards and done flags gathered to rank 0 every `every` steps over the
+    group's backend; barrier-bracketed, max-over-ranks time.  Collective: every rank calls it."""
+    import numpy as np
+    import torch
+    from hbx import dist as hd
+    from hbx.env import OBS_KEYS, HologramVecEnv
+    vec = HologramVecEnv(mcfg, B, tsrc, pre_model_source=psrc, obs_keys=OBS_KEYS, obs_format="torch",
+                         auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9, T_PSNR_DIFF=1e9)
+    vec.reset()
+    gen = torch.Generator(device="cuda").manual_seed(13 + 7919 * hd.env_rank_world()[0])
+    n_pix = mcfg.channels * mcfg.height * mcfg.width
+    actions = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda", dtype=torch.int64)
+    buf = torch.zeros((every, 2, B), dtype=torch.float64, pin_memory=True)
+    hb = buf.numpy()
+    got = [0]
+
+    def run(k0, k1):
+        j = 0
+        for k in range(k0, k1):
+            obs, rew, dones, infos = vec.step(actions[k])
+            hb[j, 0] = rew
+            hb[j, 1] = dones
+            j += 1
+            if j == every:
+                g = hd.gather_to_rank0(buf.to(dev, non_blocking=True))
+                got[0] += 0 if g is None else g.shape[0]
+                j = 0
+        if j:
+            g = hd.gather_to_rank0(buf[:j].to(dev))
+            got[0] += 0 if g is None else g.shape[0]
+
+    run(0, warmup)
+    torch.cuda.synchronize()
+    hd.barrier()
+    got[0] = 0
+    t0 = time.perf_counter()
+    run(warmup, warmup + steps)
+    torch.cuda.synchronize()
+    hd.barrier()
+    dt = hd.max_over_ranks(time.perf_counter() - t0, dev)
+    vec.close()
+    return {"value": round(B * world * steps / dt, 2), "unit": "env-steps/s", "envs_per_rank": B, "ranks": world,
+            "steps": steps, "ms_per_step": round(dt / steps * 1e3, 4), "gather_every": every,
+            "gathered_rows_rank0": got[0],
+            "note": "HologramVecEnv.step on every rank (all five observations, numpy rewards / dones), the "
+                    "per-step rewards and done flags gathered to rank 0 every `gather_every` steps; "
+                    "barrier-bracketed, max over ranks"}
 
 
 def psnr_check(vec, N):
@@ -654,7 +887,8 @@ def main():
         acc_rate = float(vec.state.flip_count.sum().item()) / float(vec.state.steps.sum().item())
         return vec, dt, timing, acc_rate
 
-    ranks_seen = hd.describe_world(dev)
+    ranks_seen = hd.describe_devices(dev)
+    n_devices = check_devices(ranks_seen, world, rehearse, dev)
     vec, dt, timing, acc_rate = measure("fft", args.steps, args.warmup)
     value = B * world * args.steps / dt
     ms_per_step = dt / args.steps * 1e3
@@ -686,7 +920,7 @@ def main():
                       f"env-steps/sec ({N}x{N} crop of 1024x1024, 24-plane)",
             "value": round(value, 2),
             "unit": "env-steps/s",
-            "n_gpus": world,
+            "n_gpus": n_devices if rehearse else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -706,6 +940,8 @@ def main():
                                    "truncated stay on the device, HologramVecEnv(obs_keys=())); the SB3-facing "
                                    "step with all five observations is `vecenv_step_obs`"},
             "ranks_seen": ranks_seen,
+            "ranks_seen_note": "[rank, world, local_rank, backend, current device, PCI address, uuid] from "
+                               "every rank (hbx.dist.describe_devices): the GPU each rank actually ran on",
             "roofline": roofline,
             "passes": rounded(passes),
             "step_alg_GBs": round(step_bytes / (ms_per_step * 1e-3) / 1e9, 1),
@@ -719,6 +955,10 @@ def main():
                         "step_alg_frac"},
             "accept_rate": round(acc_rate, 4),
         }
+        if rehearse:
+            out["rehearsal"] = True
+            out["rehearsal_note"] = (f"HBX_BENCH_REHEARSE_ONE_GPU=1: {world} ranks time-sharing {n_devices} GPU(s) "
+                                     "over gloo -- exercises the world > 1 code path, NOT a scaling measurement")
         if world == 1 and not args.no_psnr_check:
             out["psnr_delta_vs_numpy"] = psnr_check(vec, N)
     dbs_mask = vec.state.mask[0].clone()
@@ -824,18 +1064,19 @@ def main():
                         "(csrc/hbx_passes896.hip)"}
         torch.cuda.empty_cache()
 
-    if world == 1 and not args.no_ppo:
-        # SURVEY 3.2 / BASELINE cfg 4's per-GPU shard: train-PPO.py's env (env.py, 256x256x8 mono),
-        # 128 envs per GPU, FFT mode -- a secondary line, not the headline metric
+    if not args.no_ppo:
+        # SURVEY 3.2 / BASELINE configs[3]'s per-GPU shard: train-PPO.py's env (env.py, 256x256x8
+        # mono), 128 envs per GPU, FFT mode -- a secondary line, not the headline metric; at world > 1
+        # every rank steps its own 128 envs and the metrics are gathered to rank 0 (train-PPO.py:275-322)
         mono = mono_config(256)
         # a 0.35-ms step: 8x the headline's step count keeps the timed region ~0.1 s
         msteps = 8 * args.steps
         vec, dt, timing, acc_rate = measure("fft", msteps, args.warmup, mcfg=mono)
         ps = pass_table(timing, algorithmic_bytes(256, mono.planes))
         vec.close()
+        mono_ms = dt / msteps * 1e3
         if rank == 0:
             dom = max(ps, key=lambda n: ps[n]["avg_ms"])
-            mono_ms = dt / msteps * 1e3
             pmc = load_pmc_traffic(256)
             mtraffic = None
             if pmc and dom in pmc.get("kernels", {}):
@@ -843,7 +1084,8 @@ def main():
                 if kinfo.get("jobs_per_launch") == ps[dom]["jobs_per_launch"] and kinfo.get("N") == 256:
                     mtraffic = kinfo.get("hbm_bytes_per_launch")
             out["ppo_mono_256"] = {
-                "value": round(B * msteps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": msteps,
+                "value": round(B * world * msteps / dt, 2), "unit": "env-steps/s", "envs": B,
+                "global_envs": B * world, "n_ranks": world, "steps": msteps,
                 "ms_per_step": round(mono_ms, 4), "accept_rate": round(acc_rate, 4),
                 "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ps[dom]["achieved_GBs"], 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -854,37 +1096,60 @@ def main():
                              "kernel_avg_ms": round(ps[dom]["avg_ms"], 4)},
                 "passes": rounded(ps),
                 "note": "configs[0] / train-PPO.py's env (env.py, 256x256, 1 colour group x 8 planes at 515 nm), "
-                        "128 envs per GPU, FFT mode, same env semantics as the headline"}
-            if not args.no_obs:
-                out["ppo_mono_256"]["vecenv_step_obs"] = vecenv_step_obs(
-                    mono, B, msteps, args.warmup,
-                    lambda i: target_source(i)[:1, :256, :256].contiguous(),
-                    lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12)
-                out["ppo_mono_256"]["vecenv_step_obs"]["graph_replay"] = {k: v for k, v in vecenv_step_obs(
-                    mono, B, msteps, args.warmup,
-                    lambda i: target_source(i)[:1, :256, :256].contiguous(),
-                    lambda i: pre_model_source(i)[:8, :256, :256].contiguous(), mono_ms, 12,
-                    graph=True).items() if k in ("value", "ms_per_step", "obs_overhead_frac")}
-            if args.cpu_sample > 0:
-                out["ppo_mono_256"]["cpu_baseline"] = cpu_baseline_mono(max(40, 25 * args.cpu_sample))
+                        "128 envs per GPU, FFT mode, same env semantics as the headline" +
+                        (f"; {world} ranks, metric gather to rank 0 every {args.gather_every} steps" if world > 1 else "")}
+        if not args.no_obs:
+            mt = lambda i: target_source(i)[:1, :256, :256].contiguous()   # noqa: E731
+            mp = lambda i: pre_model_source(i)[:8, :256, :256].contiguous()  # noqa: E731
+            if world == 1:
+                if rank == 0:
+                    vo = vecenv_step_obs(mono, B, msteps, args.warmup, mt, mp, mono_ms, 12)
+                    vo["graph_replay"] = {k: v for k, v in vecenv_step_obs(
+                        mono, B, msteps, args.warmup, mt, mp, mono_ms, 12,
+                        graph=True).items() if k in ("value", "ms_per_step", "obs_overhead_frac")}
+                    vo["lazy_obs_unread"] = {k: v for k, v in vecenv_step_obs(
+                        mono, B, msteps, args.warmup, mt, mp, mono_ms, 12,
+                        obs_format="lazy").items() if k in ("value", "ms_per_step", "obs_overhead_frac",
+                                                            "overhead_vs_pure_device_step")}
+                    out["ppo_mono_256"]["vecenv_step_obs"] = vo
+            else:
+                vo = vecenv_step_sharded(mono, B, msteps, args.warmup, mt, mp, args.gather_every, dev, world)
+                if rank == 0:
+                    out["ppo_mono_256"]["vecenv_step_obs"] = vo
+        if rank == 0 and world == 1 and args.cpu_sample > 0:
+            out["ppo_mono_256"]["cpu_baseline"] = cpu_baseline_mono(max(40, 25 * args.cpu_sample))
         if not args.no_planes:      # the same mono step in the plane-cached FFT mode (bit-exact)
             vec, dt, timing, _ = measure("planes", msteps, args.warmup, mcfg=mono)
             vec.close()
             if rank == 0:
                 pps = pass_table(timing, plane_cached_bytes(256, mono.planes))
                 out["ppo_mono_256"]["plane_cached_mode"] = {
-                    "value": round(B * msteps / dt, 2), "unit": "env-steps/s",
+                    "value": round(B * world * msteps / dt, 2), "unit": "env-steps/s",
                     "ms_per_step": round(dt / msteps * 1e3, 4),
-                    "vs_fft_mode": round((B * msteps / dt) / out["ppo_mono_256"]["value"], 3),
+                    "vs_fft_mode": round((B * world * msteps / dt) / out["ppo_mono_256"]["value"], 3),
                     "passes": rounded(pps)}
+
+    if rank == 0 and world == 1 and not args.no_dropin:
+        # configs[0] on the GPU: the drop-in single env an unchanged train-PPO.py binds, beside the
+        # reference's algorithm on torch.fft and an unchanged DBS.py-style shim caller
+        d = dropin_env(256, 1, max(1000, 20 * args.steps), 50)
+        d["torch_reference_step"] = torch_reference_step(256, 300, 20)
+        d["shim_dbs_loop"] = shim_dbs_loop(256, 300, 20)
+        cb = out.get("ppo_mono_256", {}).get("cpu_baseline")
+        if cb:
+            d["cpu_baseline_mono"] = {"value": cb["value"], "unit": cb["unit"], "cores": cb["cores"],
+                                      "vs_dropin": round(d["value"] / cb["value"], 1)}
+        out["dropin_env_256"] = d
+        out["dropin_env_1024x24"] = dropin_env(1024, 3, 60, 5)
+        torch.cuda.empty_cache()
 
     if rank == 0:
         if world == 1 and args.cpu_sample > 0:
             out["cpu_baseline"] = cpu_baseline(args.cpu_sample, N)
             if not args.no_scipy:
                 try:
-                    workers = min(16, len(os.sched_getaffinity(0)))
-                    out["cpu_baseline_scipy"] = cpu_baseline_scipy(max(4, args.cpu_sample), N, workers)
+                    workers = min(16, host_cpus())
+                    out["cpu_baseline_scipy"] = cpu_baseline_scipy(max(20, args.cpu_sample), N, workers)
                 except Exception as e:  # scipy is optional on the box
                     out["cpu_baseline_scipy"] = {"error": str(e)}
         print(json.dumps(out), file=json_out, flush=True)

@@ -173,8 +173,10 @@ __global__ void k_env_step_finalize(const JobDesc* __restrict__ jobs,
     if (b >= n) return;
     js = job_stats + 3 * (size_t)b;
   }
-  // the error word is final here (k_jobs_from_actions, the only kernel of the step that sets it,
-  // ran before): mirror it next to the step outputs (ABI v11)
+  // the error word is final here: every kernel of the step that sets it (k_jobs_from_actions, or
+  // at N = 1024 / 256 the fused first pass's decode) ran before this one.  Mirror it next to the
+  // step outputs (ABI v11); a later error source must run before this kernel, which stays the
+  // last one of the step that reads the word
   if (b == 0 && env.error_host) env.error_host[0] = env.error ? env.error[0] : 0;
   const JobDesc jb = jobs[b];
   if (delta_out) delta_out[b] = NAN;   // no importance lookup for an invalid job

@@ -958,12 +958,9 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
   if constexpr (!PERSIST) {
     return;
   } else {
-    // a waiting block that timed out stored fault = done = 1 with sc1 stores; the state this
-    // block built came from the batch start (fault 0), so re-read the abort word and keep them
-    if (tid == 0 && __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      s_ws.fault = 1;
-      s_ws.done = 1;
-    }
+    // a waiting block that times out raises the abort word (and stores fault = done = 1, which
+    // this block's state store below may overwrite): k_walk_abort_fold, queued behind the
+    // launch, folds the abort word into the state after every block has finished
     __syncthreads();
     if (tid < kWsWords)
       __builtin_amdgcn_raw_buffer_store_b32(reinterpret_cast<const unsigned*>(&s_ws)[tid], r_ws, tid * 4, 0, kSc1);
@@ -981,6 +978,15 @@ __global__ __launch_bounds__(kWalkNT) void k_walk_step(WalkArgs a, int* __restri
     __syncthreads();
   }
   }   // batch loop
+}
+
+// after a persistent launch: a timed-out grid barrier (abort word) marks the walk state faulted
+// and done, whatever the deciding block stored last (runs once the grid has drained)
+__global__ void k_walk_abort_fold(const int* abort_word, hbx_dbs_walk_t* w) {
+  if (threadIdx.x == 0 && *abort_word) {
+    w->fault = 1;
+    w->done = 1;
+  }
 }
 
 // blocks per candidate: enough blocks in flight to stream at full rate for
@@ -1046,7 +1052,12 @@ hipError_t launch_walk(const PlanDev& pd, const WalkLaunch& l, hipStream_t st) {
         case 3: fn = reinterpret_cast<const void*>(&k_walk_step<3, true, true>); break;
         default: fn = reinterpret_cast<const void*>(&k_walk_step<4, true, true>); break;
       }
-      if (hipLaunchCooperativeKernel(fn, grid, dim3(kWalkNT), args, 0, st) == hipSuccess) return hipSuccess;
+      if (hipLaunchCooperativeKernel(fn, grid, dim3(kWalkNT), args, 0, st) == hipSuccess) {
+        // the abort word goes into the walk state only once the whole grid has drained (stream
+        // order): a decider that stored its state after a waiter's timeout cannot hide it
+        hipLaunchKernelGGL(k_walk_abort_fold, dim3(1), dim3(64), 0, st, l.counter + kWalkAbort, l.walk);
+        return hipGetLastError();
+      }
       (void)hipGetLastError();
     }
     for (int b = 0; b < l.batches; ++b) {

@@ -279,11 +279,7 @@ class _Walk:
         slot = self.done_n % 2
         self.events[slot].synchronize()
         self.done_n += 1
-        st = _lib.DbsWalk.from_buffer_copy(self.pinned[slot].numpy().tobytes())
-        if st.fault:   # a persistent walk launch's grid barrier timed out (hbx.h: fault)
-            raise RuntimeError("hbx_dbs_walk_psf: persistent walk barrier timed out; walk state unreliable "
-                               "(rerun with HBX_WALK_PERSIST=0)")
-        return st
+        return walk_state(self.pinned[slot].numpy().tobytes())
 
     def advance(self):
         """Wait for the oldest chunk in flight, act on its state, refill."""
@@ -481,6 +477,17 @@ def _greedy_walk(plan: Plan, mask, target, order_t, total, stop_diff, k_min, k_m
 _STREAMS = {}
 
 
+def walk_state(raw: bytes) -> "_lib.DbsWalk":
+    """The hbx_dbs_walk_t a walk chunk left (read back through pinned memory); raises when
+    the state is faulted -- a persistent launch's grid barrier timed out (hbx.h: fault; the
+    abort word is folded into the state once the grid has drained, k_walk_abort_fold)."""
+    st = _lib.DbsWalk.from_buffer_copy(raw)
+    if st.fault:
+        raise RuntimeError("hbx_dbs_walk_psf: persistent walk barrier timed out; walk state unreliable "
+                           "(rerun with HBX_WALK_PERSIST=0)")
+    return st
+
+
 def _walk_stream(device, i: int):
     """The stream of side-by-side walk i.  Default: a fresh torch stream per walk per call
     (measured at 1024x24, 32,768 candidates per image: 2 walks 95k, 3 walks 178k, 4 walks
@@ -545,7 +552,7 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
 
 
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
-           k_min: int = 4, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
+           k_min: Optional[int] = None, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
            stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None,
            graphs: bool = False, planes: Optional[bool] = None, device_walk: Optional[bool] = None) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
@@ -564,7 +571,12 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     mode="psf_host": the same candidates through hbx_eval_flips_psf /
     hbx_commit_flip_psf with a host decision per batch.
     progress(pos, accepted, prev_psnr, seconds): optional callback per chunk of
-    the device walk (mode="psf")."""
+    the device walk (mode="psf").
+    k_min / k_max bound the speculation depth K (candidates per batch): the device walks pick K
+    from the running acceptance rate within [k_min (default 1), k_max]; host-decided batches
+    (device_walk=False, mode="psf_host") grow K from k_min (default 4).  graphs=True replays the
+    incremental walk's chunks from HIP graphs (mode="psf"); the FFT-mode device walk has no
+    graph variant and refuses it."""
     if mode not in ("fft", "psf", "psf_host"):
         raise ValueError(f"mode must be 'fft', 'psf' or 'psf_host', got {mode!r}")
     dev = plan.device
@@ -577,7 +589,7 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     if mode == "psf":
         order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
         total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
-        return _greedy_walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
+        return _greedy_walk(plan, mask, target, order_t, total, stop_diff, k_min or 1, k_max or _lib.WALK_MAX_K,
                             stream, refresh_every, progress=progress, graphs=graphs)
     mode = "psf" if mode == "psf_host" else mode
     k_max = min(k_max or plan.max_jobs, plan.max_jobs)
@@ -592,7 +604,11 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     if device_walk:
         if not planes:
             raise ValueError("device_walk=True runs on the plane cache (planes=True)")
-        w = _PlanesWalk(plan, mask, target, order_t, total, stop_diff, 1, k_max, stream, 0, progress=progress)
+        if graphs:
+            raise ValueError("graphs=True: the FFT-mode device walk has no graph variant (device_walk=False "
+                             "for host-decided batches, or mode='psf')")
+        w = _PlanesWalk(plan, mask, target, order_t, total, stop_diff, k_min or 1, k_max, stream, 0,
+                        progress=progress)
         while not w.finished:
             w.advance()
         return w.result()
@@ -616,7 +632,7 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     psnr_buf = torch.empty(k_max, dtype=torch.float64, device=dev)
     gst_buf = torch.empty((k_max, 3), dtype=torch.float64, device=dev)
     kdev = torch.empty(1, dtype=torch.int32, device=dev)
-    ctl = KController(k_min=k_min, k_max=k_max, k0=min(16, k_max))
+    ctl = KController(k_min=4 if k_min is None else k_min, k_max=k_max, k0=min(16, k_max))
     pos, launches = 0, 0
     acc_pos, acc_psnr, acc_t = [], [], []
     stopped = False

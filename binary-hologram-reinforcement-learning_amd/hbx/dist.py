@@ -177,6 +177,61 @@ def describe_world(device=None) -> List[List]:
     return [[int(a), int(b), int(c), be] for a, b, c in allr.cpu().tolist()]
 
 
+_ID_BYTES = 64      # pci id (16 B) + uuid (48 B) per rank, as 8 int64 words
+
+
+def device_identity(device=None) -> Tuple[int, str, str]:
+    """(torch.cuda.current_device(), PCI address "dddd:bb:dd", uuid) of the GPU this process
+    actually runs on; (-1, "cpu", "") without one.  HIP_VISIBLE_DEVICES can renumber the
+    devices of a process (every rank may see its GPU as index 0), so the PCI address and the
+    uuid are what tell two ranks' GPUs apart."""
+    if device is not None and torch.device(device).type != "cuda":
+        return -1, "cpu", ""
+    if not torch.cuda.is_available():
+        return -1, "cpu", ""
+    cur = torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(cur)
+    pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return cur, pci, str(getattr(p, "uuid", ""))
+
+
+def _id_words(pci: str, uuid: str) -> List[int]:
+    raw = pci.encode()[:16].ljust(16, b"\0") + uuid.encode()[:48].ljust(48, b"\0")
+    return [int.from_bytes(raw[i:i + 8], "little", signed=True) for i in range(0, _ID_BYTES, 8)]
+
+
+def _id_strings(words: List[int]) -> Tuple[str, str]:
+    raw = b"".join(int(w).to_bytes(8, "little", signed=True) for w in words)
+    return raw[:16].rstrip(b"\0").decode(errors="replace"), raw[16:].rstrip(b"\0").decode(errors="replace")
+
+
+def describe_devices(device=None) -> List[List]:
+    """[rank, world, local_rank, backend, device index, PCI address, uuid] as every rank saw
+    it, gathered to rank 0 (empty elsewhere): the device each rank ACTUALLY used (its current
+    device), not the LOCAL_RANK it was handed.  A multi-GPU bench line carries these rows and
+    refuses to report unless they name `world` distinct GPUs (distinct_devices)."""
+    rank, world, local = env_rank_world()
+    if active():
+        rank, world = dist.get_rank(), dist.get_world_size()
+    cur, pci, uuid = device_identity(device)
+    row = torch.tensor([rank, world, local, cur] + _id_words(pci, uuid), dtype=torch.int64,
+                       device=collective_device(torch.device(device) if device is not None else None))
+    allr = gather_to_rank0(row.unsqueeze(0))
+    if allr is None:
+        return []
+    out = []
+    for r in allr.cpu().tolist():
+        p, u = _id_strings(r[4:])
+        out.append([int(r[0]), int(r[1]), int(r[2]), backend(), int(r[3]), p, u])
+    return out
+
+
+def distinct_devices(rows: List[List]) -> int:
+    """How many different GPUs the describe_devices rows name (by PCI address and uuid;
+    CPU-only ranks count as none)."""
+    return len({(r[5], r[6]) for r in rows if r[5] != "cpu"})
+
+
 def pack_step_metrics(reward: torch.Tensor, psnr: torch.Tensor, accepted: torch.Tensor,
                       terminated: torch.Tensor, truncated: torch.Tensor,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:

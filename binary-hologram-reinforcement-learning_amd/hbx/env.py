@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes as C
 import time
+import weakref
 from typing import Callable, Iterable, Optional, Sequence
 
 import numpy as np
@@ -28,6 +29,7 @@ from .plan import OpticsConfig, Plan, mono_config, pack_bits, rgb_config, unpack
 RW = 800.0   # env.py:29
 
 OBS_KEYS = ("state_record", "state", "pre_model", "recon_image", "target_image")
+STEP_OBS_KEYS = ("state_record", "state", "recon_image")   # the buffers a step rewrites
 
 # SB3's VecEnv base class when stable-baselines3 is importable (train-PPO.py:296-322 hands the
 # env to PPO; optimize_hyperparameter.py:317-318 wraps it in VecNormalize), so isinstance checks
@@ -50,19 +52,31 @@ _PARAM_ATTRS = {"max_steps": ("max_steps", int), "T_PSNR": ("t_psnr", float), "T
 class LazyObs(dict):
     """Dict observation kept on the GPU whose values become numpy arrays on first
     access (cached): an SB3 rollout buffer that reads every key pays one device ->
-    host copy per key, a consumer that reads none pays nothing.  ``.device(key)``
-    returns the device tensor without a copy.
+    host copy per key.  ``.device(key)`` returns the device tensor without a copy.
 
-    The env's observations are VIEWS of buffers the next step rewrites (ABI v8), so LazyObs
-    takes a device snapshot (clone) of every key when it is built: a key first read after
-    the next env.step() still shows this step's data (SB3 assigns self._last_obs into its
-    rollout buffer after the following step)."""
+    The env's observations are VIEWS of buffers the next step rewrites (ABI v8).  A key
+    first read after the next env.step() must still show this step's data (SB3 assigns
+    self._last_obs into its rollout buffer after the following step), so the
+    env snapshots (device clone, queued on the stream before its launches) the keys of its
+    last LazyObs that are still unread AND that the next launch rewrites: state_record /
+    state / recon_image before a step, every key before a reset.  A consumer that reads
+    every key before stepping pays no snapshot; one that reads none pays a device copy of
+    the step-mutable keys only (target / pre_model change at resets alone)."""
 
     def __init__(self, tensors: dict):
         super().__init__()
-        self._t = {k: v.clone() for k, v in tensors.items()}
+        self._t = dict(tensors)
+        self._owned = set()
         for k in self._t:
             dict.__setitem__(self, k, None)
+
+    def _snapshot(self, keys):
+        """Own a device copy of every listed key not read yet (the env calls this before it
+        launches work that rewrites those buffers)."""
+        for k in keys:
+            if k in self._t and k not in self._owned and dict.__getitem__(self, k) is None:
+                self._t[k] = self._t[k].clone()
+                self._owned.add(k)
 
     def __getitem__(self, k):
         v = dict.__getitem__(self, k)
@@ -301,11 +315,12 @@ class HologramVecEnv(_VecEnvBase):
         self._h_err = h[self._row_bytes:self._row_bytes + 4].view(np.int32)
         self._dev_index = self.device.index if self.device.type == "cuda" else None
         self._readback = torch.cuda.Event() if self.device.type == "cuda" else None
-        self._last_actions = torch.zeros(n, dtype=torch.int64, device=dev)
         self._actions = None
         self._fast_args = None
+        self._fast_ids = None
         self._settle_args = None
         self._obs_views = None
+        self._lazy_ref = None      # the last LazyObs handed out (obs_format="lazy")
         self.episode_count = 0
         if HAVE_SB3:  # pragma: no cover - SB3 absent here
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
@@ -331,10 +346,20 @@ class HologramVecEnv(_VecEnvBase):
             st.pre_model[i].copy_(pre)
         self.episode_count += 1
 
+    def _before_launch(self, keys):
+        """The last LazyObs snapshots its unread `keys` before work that rewrites them is queued."""
+        if self._lazy_ref is not None:
+            lz = self._lazy_ref()
+            if lz is None:
+                self._lazy_ref = None
+            else:
+                lz._snapshot(keys)
+
     def reset_envs(self, env_ids: Sequence[int]):
         ids = [int(i) for i in env_ids]
         if not ids:
             return
+        self._before_launch(OBS_KEYS)
         for i in ids:
             self._load_env(i)
         idt = torch.tensor(ids, dtype=torch.int32, device=self.device)
@@ -372,7 +397,9 @@ class HologramVecEnv(_VecEnvBase):
         if self.obs_format == "numpy":
             return _to_numpy(obs)
         if self.obs_format == "lazy":
-            return LazyObs(obs)
+            lz = LazyObs(obs)
+            self._lazy_ref = weakref.ref(lz)
+            return lz
         return obs
 
     # -- step --------------------------------------------------------------------
@@ -401,7 +428,7 @@ class HologramVecEnv(_VecEnvBase):
             actions = torch.where(bad, torch.full_like(a[:, 0], -1),
                                   (a[:, 0] * c.height + a[:, 1]) * c.width + a[:, 2])
         actions = actions.reshape(self.num_envs).contiguous()
-        self._last_actions = actions
+        self._before_launch(STEP_OBS_KEYS)
         if out is None:
             out = (self._reward, self._psnr, self._acc, self._term, self._trunc)
         else:
@@ -470,25 +497,37 @@ class HologramVecEnv(_VecEnvBase):
         device, the env's own output row -- as ONE ctypes call with prebuilt arguments: the
         256x8 mono step is 0.33 ms of GPU work, so the ~15 us of Python argument marshalling
         of the general path (Plan.env_step: byref / data_ptr / stream wrappers) show."""
-        if self.mode == "psf" or self.use_graph or self.action_format != "discrete" \
-                or not isinstance(actions, torch.Tensor) or actions.dtype != torch.int64 \
+        if not self._fast_ok() or not isinstance(actions, torch.Tensor) or actions.dtype != torch.int64 \
                 or actions.device != self.device or actions.numel() != self.num_envs \
                 or not actions.is_contiguous():
             return False
-        if self._fast_args is None:
+        self._launch_fast(actions.data_ptr())
+        return True
+
+    def _fast_ok(self) -> bool:
+        return self.mode != "psf" and not self.use_graph and self.action_format == "discrete"
+
+    def _launch_fast(self, actions_ptr: int):
+        """hbx_env_step on the current stream with the results written into the host-mapped
+        row; `actions_ptr` is any address the kernels can read B int64 actions from (a device
+        tensor, or host-mapped memory: BinaryHologramEnv)."""
+        self._before_launch(STEP_OBS_KEYS)
+        # the prebuilt argument list holds pointers to env.params / env.state.bufs: rebuilt when
+        # either object is replaced (ADVICE r04: a new EnvParams must not be silently ignored)
+        ids = (id(self.params), id(self.state.bufs))
+        if self._fast_args is None or self._fast_ids != ids:
             p = self.plan
             self._fast_fn = p.lib.hbx_env_step
             n, d = self.num_envs, self._hrow.device   # outputs straight into the host-mapped row
             self._fast_args = [p._h, C.byref(self.state.bufs), C.byref(self.params), n, None,
                                d, d + 8 * n, d + 16 * n, d + 17 * n, d + 18 * n, None, None]
-        self._last_actions = actions
+            self._fast_ids = ids
         a = self._fast_args
-        a[4] = actions.data_ptr()
+        a[4] = actions_ptr
         a[11] = _raw_stream(self._dev_index)
         rc = self._fast_fn(*a)
         if rc != _lib.OK:
             _lib.check(rc, "hbx_env_step")
-        return True
 
     def _settle(self):
         """HBX_OBS_SETTLE queued behind the readback event: the accepted envs' stepped group goes
@@ -674,6 +713,7 @@ class HologramVecEnv(_VecEnvBase):
         """Restore a save() of an env with the same shape; incremental mode
         re-propagates the cached fields of the restored masks exactly."""
         c, st = self.cfg, self.state
+        self._before_launch(OBS_KEYS)
         with np.load(path) as z:
             meta = tuple(int(v) for v in z["meta"])
             if meta != (c.height, c.width, c.groups, c.planes, self.num_envs):
@@ -765,6 +805,29 @@ class BinaryHologramEnv(spaces.EnvBase):
     (env.py:135-140,176-181) -- and ``observation_space.contains`` accepts them;
     scalars are Python floats.
 
+    What a step moves (the reference: the whole mask H2D, the recon D2H, a PSNR sync,
+    env.py:170-179).  The propagation, PSNR, reward and rollback run on the GPU
+    (hbx_env_step, the batched env at B = 1); the host keeps numpy MIRRORS of what the
+    reference keeps on the host, updated by the same rules:
+
+    * ``state`` / ``state_record`` are numpy int8 (1, CH, N, N) arrays built at reset
+      (env.py:120-121) and changed by the one byte a step touches -- obs["state"] and
+      obs["state_record"] ARE these arrays (env.py:176-177 hands out self.state itself, so
+      a rolled-back step's obs shows the rolled-back state);
+    * ``observation`` (pre_model) and ``target_image_np`` are copied once per reset and
+      handed out as the same arrays every step (env.py:107,111,178,180);
+    * steps / flip_count / psnr_sustained_steps / previous_psnr / max_psnr_diff follow
+      env.py:155-258 on the host from the step's psnr and accept flag;
+    * the action is written into host-mapped memory the step kernels read directly (no
+      H2D copy); the kernels write reward / psnr / accept / terminate / truncate and the
+      error word into host-mapped memory; recon_image (a fresh array every step, as
+      ``result_after.cpu().numpy()``) is copied D2H into pinned memory behind the step.
+
+    One blocking wait per step (``host_syncs`` counts them).  The device mask is the
+    authority for the physics: writing into obs["state"] does not reach the GPU (the
+    reference's DBS drivers mutate it only to run their own tt.simulate loop, never
+    calling step() on the edited state, DBS.py:218-294).
+
     verbose=True (the default, as the reference always prints) gives the reference's
     console lines (env.py:100,104,142-145:
     episode start, initial PSNR / MSE; :203-246: a Step block at every 0.01 dB
@@ -779,6 +842,10 @@ class BinaryHologramEnv(spaces.EnvBase):
                  device: Optional[int] = None, debug_timing: bool = False, **vec_kwargs):
         super().__init__()
         self.cfg = config or mono_config(256)
+        if vec_kwargs.get("mode", "fft") == "psf":
+            raise ValueError("BinaryHologramEnv returns the stepped recon_image (env.py:179): mode 'fft' or 'planes'")
+        if "obs_keys" in vec_kwargs:
+            raise ValueError("BinaryHologramEnv always returns the reference's five observation keys")
         self.target_function = target_function
         self.trainloader = trainloader
         self.data_iter = iter(self.trainloader)
@@ -786,15 +853,29 @@ class BinaryHologramEnv(spaces.EnvBase):
         self.verbose = verbose
         self.debug_timing = debug_timing
         self.current_file = None
+        # the device keeps only what the host cannot derive: the stepped recon (state / record /
+        # pre_model / target are host mirrors, see the class docstring)
         self._vec = HologramVecEnv(self.cfg, 1, self._next_target, self._pre_model, max_steps=max_steps,
                                    T_PSNR=T_PSNR, T_steps=T_steps, T_PSNR_DIFF=T_PSNR_DIFF,
-                                   auto_reset=False, device=device, **vec_kwargs)
+                                   auto_reset=False, device=device, obs_keys=("recon_image",), **vec_kwargs)
         self.observation_space = self._vec.observation_space
         self.action_space = self._vec.action_space
         self.num_pixels = self._vec.num_pixels
+        c = self.cfg
+        self._recon_shape = (1, c.groups, c.height, c.width)
+        # the action as the step kernels read it: host-mapped memory (hbx_host_alloc)
+        self._act_row = HostRow(self._vec.plan.lib, 8)
+        self._act = self._act_row.array.view(np.int64)
+        self._act_dev = None          # device copy, for the step paths that take a tensor (graph replay)
+        self.host_syncs = 0           # blocking waits in step() (one per step)
         self.episode_num_count = 0
         self.initial_psnr = None
         self.previous_psnr = None
+        self.state = None
+        self.state_record = None
+        self.observation = None
+        self.target_image_np = None
+        self._tgt_in = self._pre_out = None
         self.steps = 0
         self.flip_count = 0
         self.psnr_sustained_steps = 0
@@ -814,23 +895,13 @@ class BinaryHologramEnv(spaces.EnvBase):
         if self.verbose:                                               # env.py:104
             print(f"\033[40;93m[Episode Start] Currently using dataset file: {self.current_file}, "
                   f"Episode count: {self.episode_num_count}\033[0m")
+        self._tgt_in = target
         return target
 
     def _pre_model(self, target):
         out = self.target_function(target)
-        self.observation = out
+        self._pre_out = out
         return out
-
-    @property
-    def state(self):
-        sb = self._vec.state.state_bytes
-        bits = sb[0] if sb is not None else unpack_bits(self._vec.state.mask[0], self.cfg.width)
-        return bits.unsqueeze(0).cpu().numpy()
-
-    def _obs(self, stepped: bool) -> dict:
-        """The B = 1 batch axis of HologramVecEnv.observe() removed: (1, CH, N, N) /
-        (1, G, N, N) numpy arrays, the reference's obs dict (env.py:135-140,176-181)."""
-        return {k: v[0] for k, v in _to_numpy(self._vec.observe(stepped=stepped)).items()}
 
     def _mse(self) -> float:
         """tt.relativeLoss(result, target, F.mse_loss) of the current state (env.py:131)."""
@@ -843,9 +914,18 @@ class BinaryHologramEnv(spaces.EnvBase):
 
     def reset(self, seed=None, options=None):
         self.episode_num_count += 1
-        self.psnr_sustained_steps = 0
-        obs = {k: v[0] for k, v in _to_numpy(self._vec.reset()).items()}
-        self.initial_psnr = float(self._vec.state.init_psnr[0].item())
+        c = self.cfg
+        self._vec.reset_envs([0])
+        # the host mirrors (env.py:107,111,120-121): the same float32 values the device took
+        host = lambda t: torch.as_tensor(t).detach().to("cpu", torch.float32).numpy()   # noqa: E731
+        self.target_image_np = np.ascontiguousarray(host(self._tgt_in)).reshape(1, c.groups, c.height, c.width)
+        self.observation = np.ascontiguousarray(host(self._pre_out)).reshape(1, c.channels, c.height, c.width)
+        self._tgt_in = self._pre_out = None
+        self.state = (self.observation >= 0.5).astype(np.int8)
+        self.state_record = np.zeros_like(self.state)
+        st = self._vec.state
+        recon = st.recon[0:1].cpu().numpy()
+        self.initial_psnr = float(st.init_psnr[0].item())
         self.previous_psnr = self.initial_psnr
         self.steps = self.flip_count = self.psnr_sustained_steps = 0
         self.max_psnr_diff = float("-inf")
@@ -856,7 +936,9 @@ class BinaryHologramEnv(spaces.EnvBase):
             self._vec.plan.read_timing()                               # drop the reset's propagation
         self.total_start_time = time.time()
         self.step_time = time.time()
-        return obs, {"state": obs.get("state")}
+        obs = {"state_record": self.state_record, "state": self.state, "pre_model": self.observation,
+               "recon_image": recon, "target_image": self.target_image_np}
+        return obs, {"state": self.state}
 
     def _flat_action(self, action) -> int:
         return int(action)
@@ -869,73 +951,120 @@ class BinaryHologramEnv(spaces.EnvBase):
                 f"\nFlip Pixel: Channel={c}, Row={r}, Col={col}"
                 f"\nTime taken for this data: {t:.2f} seconds")
 
+    def _device_step(self, a: int) -> np.ndarray:
+        """Queue the step of action `a`, the recon readback and the settle; wait once.
+        Returns the stepped recon_image (a fresh array backed by pinned memory)."""
+        vec = self._vec
+        if vec._fast_ok():
+            self._act[0] = a                      # the previous step's kernels finished (waited below)
+            vec._launch_fast(self._act_row.device)
+        else:                                     # graph replay / MultiDiscrete: the tensor path
+            if self._act_dev is None:
+                self._act_dev = torch.zeros(1, dtype=torch.int64, device=vec.device)
+            self._act_dev.fill_(a)
+            vec.step_device(self._act_dev if vec.action_format == "discrete" else self._md_action(a))
+            vec._host_t.copy_(vec._out_raw, non_blocking=True)
+        recon = torch.empty(self._recon_shape, dtype=torch.float32, pin_memory=True)
+        recon.copy_(vec.state.recon[0:1], non_blocking=True)   # env.py:179, queued behind the step
+        vec._readback.record()
+        vec._settle()
+        vec._readback.synchronize()
+        self.host_syncs += 1
+        if vec._h_err[0]:
+            vec.state.check_error()               # clears the word and raises
+        return recon.numpy()
+
+    def _md_action(self, a: int) -> torch.Tensor:
+        c = self.cfg
+        ch, pix = divmod(a, c.height * c.width)
+        return torch.tensor([[ch, pix // c.width, pix % c.width]], dtype=torch.int64, device=self._vec.device)
+
+    def _bonus(self, ratio: float) -> float:
+        """The success / max-steps bonus the device added (for the printed Reward lines)."""
+        if self._vec.reward_kind == "importance":
+            return 100 + (-200.0 / 1500.0) * (self.steps - 1000)        # env_group.py:297-298
+        return 1828.57 * ratio ** 3 - 3733.33 * ratio ** 2 + 2800 * ratio - 595.2   # env.py:230-235
+
     def step(self, action):
         dbg = self.debug_timing
         if dbg:
             print(f"Step: {self.steps + 1:<6} | Time action: {time.time() - self.step_time:.6f} seconds")
         a = self._flat_action(action)
+        c = self.cfg
+        if not 0 <= a < self.num_pixels:
+            raise ValueError(f"action {a} outside [0, {self.num_pixels})")
         t0 = time.time()
-        reward_t, psnr_t, acc_t, term_t, trunc_t = self._vec.step_device(
-            torch.tensor([a], dtype=torch.int64, device=self._vec.device))
-        self._vec.state.check_error()                                  # syncs the step
+        recon = self._device_step(a)
         if dbg:
             print(f"Step: {self.steps + 1:<6} | Time simulate: {time.time() - t0:.6f} seconds")
         t0 = time.time()
-        obs = self._obs(stepped=True)
+        h, vec = self._vec._host_np, self._vec
+        reward = float(vec._h_rew[0])
+        psnr_after = float(h[8:16].view(np.float64)[0])
+        accepted, terminated, truncated = bool(h[16]), bool(h[17]), bool(h[18])
+        ch, pix = divmod(a, c.height * c.width)                       # env.py:157-161
+        r, col = divmod(pix, c.width)
+        self.steps += 1                                                # env.py:155
+        rec = self.state_record[0, ch, r, col:col + 1]
+        rec += 1                                                       # env.py:165 (int8, wraps)
+        obs = {"state_record": self.state_record, "state": self.state, "pre_model": self.observation,
+               "recon_image": recon, "target_image": self.target_image_np}
         if dbg:
-            print(f"Step: {self.steps + 1:<6} | Time obs: {time.time() - t0:.6f} seconds")
-        t0 = time.time()
-        st = self._vec.state
-        prev = self.previous_psnr
-        reward = float(reward_t[0].item())
-        psnr_after = float(psnr_t[0].item())
-        accepted = bool(acc_t[0].item())
-        terminated, truncated = bool(term_t[0].item()), bool(trunc_t[0].item())
-        self.steps = int(st.steps[0].item())
-        self.flip_count = int(st.flip_count[0].item())
-        self.psnr_sustained_steps = int(st.sustained[0].item())
-        self.previous_psnr = float(st.prev_psnr[0].item())
-        if dbg:
-            print(f"Step: {self.steps:<6} | Time reward: {time.time() - t0:.6f} seconds")
+            print(f"Step: {self.steps:<6} | Time obs: {time.time() - t0:.6f} seconds")
+            print(f"Step: {self.steps:<6} | Time reward: {0.0:.6f} seconds")
             print(timing_lines(self.steps, self._vec.plan.read_timing()))
         if not accepted:                                               # env.py:191-196 (rolled back on the device)
             if dbg:
                 print(f"Step: {self.steps:<6} | Time rollback: {0.0:.6f} seconds")
                 self.step_time = time.time()
             return obs, reward, False, False, {}
+        self.state[0, ch, r, col] ^= 1                                 # env.py:164, kept
+        self.flip_count += 1                                           # env.py:167
+        prev = self.previous_psnr
         change, diff = psnr_after - prev, psnr_after - self.initial_psnr
-        self.max_psnr_diff = max(self.max_psnr_diff, diff)
-        ratio = self.flip_count / self.steps if self.steps > 0 else 0
-        c, r, col = (int(v) for v in np.unravel_index(a, (self.cfg.channels, self.cfg.height, self.cfg.width)))
-        base_reward = change * self._vec.params.reward_weight
+        self.max_psnr_diff = max(self.max_psnr_diff, diff)            # env.py:198
+        ratio = self.flip_count / self.steps if self.steps > 0 else 0  # env.py:200
+        base_reward = change * vec.params.reward_weight if vec.reward_kind == "psnr" else reward
         t0 = time.time()
         while self.next_print_thresholds and psnr_after >= self.next_print_thresholds[0]:   # env.py:203-212
             self.next_print_thresholds.pop(0)
             if self.verbose:
-                print(self._block(psnr_after, change, diff, base_reward, ratio, c, r, col))
+                print(self._block(psnr_after, change, diff, base_reward, ratio, ch, r, col))
+        self.previous_psnr = psnr_after                                # env.py:214
         if dbg:
             print(f"Step: {self.steps:<6} | Time print: {time.time() - t0:.6f} seconds")
         t0 = time.time()
         bonus = 0.0
         if diff >= self.T_PSNR_DIFF or (psnr_after >= self.T_PSNR and diff < 0.1):          # env.py:216-235
             if self.verbose:
-                print(self._block(psnr_after, change, diff, base_reward, ratio, c, r, col))
+                print(self._block(psnr_after, change, diff, base_reward, ratio, ch, r, col))
+            self.psnr_sustained_steps += 1                             # env.py:225
             if self.psnr_sustained_steps >= self.T_steps and diff >= self.T_PSNR_DIFF:
-                bonus = reward - base_reward
+                bonus = self._bonus(ratio)
         if dbg:
             print(f"Step: {self.steps:<6} | Time diff: {time.time() - t0:.6f} seconds")
         t0 = time.time()
         if self.steps >= self.max_steps and self.verbose:                                   # env.py:237-246
-            print(self._block(psnr_after, change, diff, base_reward + bonus, ratio, c, r, col))
+            print(self._block(psnr_after, change, diff, base_reward + bonus, ratio, ch, r, col))
         if dbg:
             print(f"Step: {self.steps:<6} | Time max_steps: {time.time() - t0:.6f} seconds")
             print(f"Step: {self.steps:<6} | Time terminated: {0.0:.6f} seconds")
             self.step_time = time.time()
         return obs, reward, terminated, truncated, {}
 
+    def device_counters(self) -> dict:
+        """The device's own copy of the episode counters (steps, flip_count, sustained,
+        previous psnr) -- the host mirrors must equal these (tests/test_gpu_dropin.py)."""
+        st = self._vec.state
+        return {"steps": int(st.steps[0].item()), "flip_count": int(st.flip_count[0].item()),
+                "psnr_sustained_steps": int(st.sustained[0].item()),
+                "previous_psnr": float(st.prev_psnr[0].item()),
+                "max_psnr_diff": float(st.max_psnr_diff[0].item())}
+
     def close(self):
         self._vec.close()
-
+        self._act = None
+        self._act_row.close()
 
 class BinaryHologramEnvGroup(BinaryHologramEnv):
     """Drop-in for env_group.py's ``BinaryHologramEnv`` (env_group.py:37-320):

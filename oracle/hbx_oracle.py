@@ -330,7 +330,12 @@ class OracleEnv:
         st[g] = chan_stats(ig, self.target[g])
         return self.prop.psnr(st), g, ig, st
 
-    def step(self, action: int) -> StepResult:
+    def step(self, action: int, accept: Optional[bool] = None) -> StepResult:
+        """env.py:154-259.  ``accept`` (tests only) overrides the rollback decision -- to
+        follow the device's decision at a change below f32 resolution, where an f32 and an
+        f64 propagation can order a near-tie differently; the caller asserts the rule's own
+        decision wherever the change is clear of that resolution.  ``last_change`` and
+        ``last_group_intensity`` keep the change and the stepped group's intensity."""
         c = self.cfg
         self.steps += 1                                                # env.py:155
         ch, r, col = (int(v) for v in decode_action(action, c.height, c.width))
@@ -339,8 +344,11 @@ class OracleEnv:
         psnr_after, g, ig, st = self.evaluate_flip(action)
         psnr_change = psnr_after - self.previous_psnr                  # env.py:184
         psnr_diff = psnr_after - self.initial_psnr                     # env.py:185
+        self.last_change, self.last_group_intensity = psnr_change, (g, ig)
         reward = psnr_change * RW                                      # env.py:188
         reject = (psnr_change < 0) if self.accept_rule == 0 else not (psnr_change > 0)
+        if accept is not None:
+            reject = not accept
         if reject:                                                     # env.py:191-196
             self.flip_count -= 1
             return StepResult(action, psnr_after, reward, False, False, False)

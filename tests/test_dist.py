@@ -42,10 +42,11 @@ def _worker(rank, world, port, out):
         mg.add(reward + k, psnr, acc, term, trunc)
     mg.flush()
     seen = hd.describe_world()
+    devs = hd.describe_devices()
     hd.barrier()
     if rank == 0:
         blocks = [b.tolist() for b in mg.gathered]
-        out.put((g.tolist(), hist.tolist(), mx, (lo, hi), blocks, seen))
+        out.put((g.tolist(), hist.tolist(), mx, (lo, hi), blocks, seen, devs))
     else:
         assert g is None
         out.put(None)
@@ -64,8 +65,10 @@ def test_gloo_world2_gather_and_reduce():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    g, hist, mx, (lo, hi), blocks, seen = next(r for r in res if r is not None)
+    g, hist, mx, (lo, hi), blocks, seen, devs = next(r for r in res if r is not None)
     assert seen == [[0, 2, 0, "gloo"], [1, 2, 1, "gloo"]]
+    # no GPU here: both ranks report the host, which names no GPU at all
+    assert devs == [[0, 2, 0, "gloo", -1, "cpu", ""], [1, 2, 1, "gloo", -1, "cpu", ""]]
     assert [len(b) for b in blocks] == [6, 4]                  # world * steps per gather
     for b, steps in zip(blocks, ([0, 1, 2], [3, 4])):
         for r in range(2):
@@ -226,3 +229,25 @@ def test_forced_world1_group_runs_every_collective():
     assert plain[3] == [[0, 1, 0, "none"]] and forced[3] == [[0, 1, 0, "gloo"]]
     assert [len(b) for b in forced[0]] == [2, 1]
     assert plain[:3] == forced[:3] and plain[4:] == forced[4:]
+
+
+def test_distinct_devices_and_bench_refusal(monkeypatch):
+    """A multi-GPU bench line must prove it ran on N distinct GPUs: rows
+    naming the same PCI address / uuid twice count once; bench.check_devices refuses such a
+    world outside a rehearsal and returns the distinct count inside one."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "binary-hologram-reinforcement-learning_amd")]
+    import bench
+    from hbx import dist as hd
+    assert hd._id_strings(hd._id_words("0000:75:00", "GPU-5e1f2a3b-8c9d")) == ("0000:75:00", "GPU-5e1f2a3b-8c9d")
+    two = [[0, 2, 0, "nccl", 0, "0000:75:00", "GPU-a"], [1, 2, 1, "nccl", 0, "0000:05:00", "GPU-b"]]
+    same = [[0, 2, 0, "gloo", 0, "0000:75:00", "GPU-a"], [1, 2, 1, "gloo", 0, "0000:75:00", "GPU-a"]]
+    assert hd.distinct_devices(two) == 2 and hd.distinct_devices(same) == 1
+    assert hd.distinct_devices([[0, 1, 0, "none", -1, "cpu", ""]]) == 0
+    monkeypatch.setattr(hd, "max_over_ranks", lambda x, dev=None: x)     # one process stands for the group
+    assert bench.check_devices(two, 2, False, None) == 2
+    with pytest.raises(SystemExit):
+        bench.check_devices(same, 2, False, None)
+    assert bench.check_devices(same, 2, True, None) == 1                 # a rehearsal reports 1 device
+    assert bench.check_devices([], 2, False, None) == 0                  # rank != 0: decided by rank 0

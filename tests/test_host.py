@@ -244,3 +244,32 @@ def test_env_buffers_struct_matches_header():
     names = re.findall(r"\b(\w+);", body)
     assert [f[0] for f in _lib.EnvBuffers._fields_] == names
     assert C.sizeof(_lib.EnvBuffers) == 8 * (len(names) - 2) + 4 * 2   # two int32 fields
+
+
+def test_walk_state_fault_plumbing():
+    """A persistent walk whose grid barrier timed out leaves fault = done = 1 in the walk state
+    (k_walk_abort_fold, after the grid has drained): the host reader raises on it and passes a
+    clean state through unchanged (hbx.dbs.walk_state)."""
+    import ctypes as C
+    import pytest
+    from hbx import _lib
+    from hbx.dbs import walk_state
+    w = _lib.DbsWalk()
+    w.pos, w.accepted, w.done = 17, 5, 0
+    st = walk_state(bytes(w))
+    assert (st.pos, st.accepted, st.fault, st.done) == (17, 5, 0, 0)
+    w.fault, w.done = 1, 1
+    with pytest.raises(RuntimeError, match="barrier timed out"):
+        walk_state(bytes(w))
+    assert C.sizeof(_lib.DbsWalk) == len(bytes(w))
+
+
+def test_dropin_env_rejects_unsupported_modes_before_device_work():
+    """BinaryHologramEnv returns the stepped recon_image (env.py:179): the incremental mode
+    (which has none) and a caller-chosen obs_keys are refused from the arguments alone."""
+    import pytest
+    from hbx.env import BinaryHologramEnv
+    with pytest.raises(ValueError, match="recon_image"):
+        BinaryHologramEnv(lambda t: t, [], mode="psf")
+    with pytest.raises(ValueError, match="five observation keys"):
+        BinaryHologramEnv(lambda t: t, [], obs_keys=("state",))
