@@ -412,12 +412,109 @@ __device__ __forceinline__ uint32_t bit_transpose_level(uint32_t x, int t) {
   const uint32_t d = ((lo_v >> J) ^ hi_v) & m;
   return x ^ (hi ? d : (d << J));
 }
+// The value of lane t ^ J (J < 32) of the lane's 32-lane group, without the LDS pipe (r05): DPP
+// quad permutes for J = 1, 2, row rotations for J = 4 (two, one per half of each 8-lane run), 8,
+// and gfx950's v_permlane16_swap for J = 16.  ds_swizzle (bit_transpose_level) costs an LDS
+// round trip per level, five dependent ones per transpose (k_rowfwd32: SQ_WAIT_INST_LDS twice
+// SQ_ACTIVE_INST_LDS).  tools/lane_xor_test.hip checks every J against ds_swizzle.
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x, int t) {
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xf, 0xf, false);   // row_ror:4
+    const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x12C, 0xf, 0xf, false);   // row_ror:12
+    return (t & 4) ? a : b;
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xf, 0xf, false);   // row_ror:8
+  } else {
+    static_assert(J == 16, "lane_xor: J in {1, 2, 4, 8, 16}");
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (t & 16) ? r[0] : r[1];
+  }
+}
+
+template <int J>
+__device__ __forceinline__ uint32_t bit_transpose_level_dpp(uint32_t x, int t) {
+  constexpr uint32_t m = J == 16 ? 0x0000ffffu : J == 8 ? 0x00ff00ffu : J == 4 ? 0x0f0f0f0fu
+                       : J == 2 ? 0x33333333u : 0x55555555u;
+  const uint32_t y = lane_xor<J>(x, t);
+  const bool hi = (t & J) != 0;
+  const uint32_t lo_v = hi ? y : x, hi_v = hi ? x : y;
+  const uint32_t d = ((lo_v >> J) ^ hi_v) & m;
+  return x ^ (hi ? d : (d << J));
+}
+
+// 32 x 32 bit transpose across a 32-lane group: bit r of lane t's result = bit t of lane r's x
 __device__ __forceinline__ uint32_t group_bit_transpose(uint32_t x, int t) {
+  x = bit_transpose_level_dpp<16>(x, t);
+  x = bit_transpose_level_dpp<8>(x, t);
+  x = bit_transpose_level_dpp<4>(x, t);
+  x = bit_transpose_level_dpp<2>(x, t);
+  return bit_transpose_level_dpp<1>(x, t);
+}
+// the ds_swizzle form (r02-r04), kept as the reference of tools/lane_xor_test.hip
+__device__ __forceinline__ uint32_t group_bit_transpose_swizzle(uint32_t x, int t) {
   x = bit_transpose_level<16>(x, t);
   x = bit_transpose_level<8>(x, t);
   x = bit_transpose_level<4>(x, t);
   x = bit_transpose_level<2>(x, t);
   return bit_transpose_level<1>(x, t);
+}
+
+// ---------------------------------------------------------------------------
+// Mirror-paired lane order of k_rowfwd32's second FFT stage (r05).  The Hermitian split needs
+// conj Z[N - k] next to Z[k]; with lane t holding k1 = t (k = k1 + 32 k2) the partner lane is
+// 32 - t: a cross-lane gather (two ds_bpermute per value, 32 per row block).  Reading column
+// k1 = kMirrorK1[t] of the transposed tile instead puts k1 and 32 - k1 on the lane pair
+// (2m, 2m + 1): the partner is lane t ^ 1, a DPP quad permute.  Lanes 0 / 1 hold k1 = 0 / 16,
+// their own mirrors.  Which pair sits in which half of the group is chosen so the plane tile's
+// lane-row writes (tile_pos<32, 8> of line k1 + 32 k2) stay conflict-free for the 16-lane
+// service of ds_write_b64 (tools/lds_swizzle_model.py mirror_pair_order, exhaustive over splits).
+static __constant__ const int kMirrorK1[32] = {0, 16, 1, 31, 3, 29, 4, 28, 5, 27, 7, 25, 8, 24, 12, 20,
+                                               2, 30, 6, 26, 9, 23, 10, 22, 11, 21, 13, 19, 14, 18, 15, 17};
+__device__ __forceinline__ int mirror_k1(int t) { return kMirrorK1[t & 31]; }
+
+// fft_group_split (R = 32, packed) with the second stage in mirror-paired lane order: lane t
+// ends up holding X[k1 + 32 k2] for k1 = mirror_k1(t) (passed in), k2 = 0..31.
+template <bool INV, class T>
+__device__ __forceinline__ void fft_group_split_mirror(T (&v)[32], int t, int k1, float* sc, const float2* tw) {
+  asm volatile("" ::: "memory");
+  dft_reg<32, INV>(v);
+#pragma unroll
+  for (int j = 1; j < 32; ++j) {
+    const pk2 w = to_pk(tw[j * 32 + t]);
+    v[j] = st_pk<T>(INV ? pk_cmulc(ld_pk(v[j]), w) : pk_cmul(ld_pk(v[j]), w));
+  }
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < 32; ++j) sc[t * 33 + j] = v[j].x;
+  wave_sync();
+#pragma unroll
+  for (int tt = 0; tt < 32; ++tt) v[tt].x = sc[tt * 33 + k1];
+  wave_sync();
+#pragma unroll
+  for (int j = 0; j < 32; ++j) sc[t * 33 + j] = v[j].y;
+  wave_sync();
+#pragma unroll
+  for (int tt = 0; tt < 32; ++tt) v[tt].y = sc[tt * 33 + k1];
+  wave_sync();
+  dft_reg<32, INV>(v);
+}
+
+// conj(X[N - k]) for k = k1 + 32 k2 in the mirror-paired order: lane t ^ 1's register 31 - k2
+// (DPP), lane 0 (k1 = 0) its own register (32 - k2) mod 32, lane 1 (k1 = 16) its own 31 - k2
+template <class T>
+__device__ __forceinline__ float2 mirror_conj_paired(const T (&v)[32], int k2, int t) {
+  const float2 a = make_float2(v[31 - k2].x, v[31 - k2].y);
+  float2 p;
+  p.x = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(a.x), 0xB1, 0xf, 0xf, false));
+  p.y = __uint_as_float((uint32_t)__builtin_amdgcn_mov_dpp((int)__float_as_uint(a.y), 0xB1, 0xf, 0xf, false));
+  const float2 own0 = make_float2(v[(32 - k2) & 31].x, v[(32 - k2) & 31].y);
+  const float2 z = t == 0 ? own0 : (t == 1 ? a : p);
+  return conjf2(z);
 }
 
 // Value of conj(X[N - k]) for k = t + R*k2, fetched from the lane group that
@@ -607,8 +704,12 @@ __device__ __forceinline__ void fft896_ns_s2(float2 (&v)[32], int t, const Scrat
 #pragma unroll
   for (int k1 = 0; k1 < 28; ++k1) *sc.at(t, k1) = v[k1];
   wave_sync();
-  // lane k1 (< 28) gathers A'[t][k1] for t = 0..31; lanes 28..31 read in-range junk
-  const int k1 = t < 28 ? t : 0;
+  // lane k1 (< 28) gathers A'[t][k1] for t = 0..31; lanes 28..31 read columns 28..31 of the
+  // padded tile (in range, never written here: don't-care values, as before).  r05: they read
+  // column 0 until r04, the same bank as lane 16 under the 16-lane service of the ds_read2_b64
+  // the compiler emits (64 extra LDS cycles per wave and transpose; k_col896's counter,
+  // tools/lds_swizzle_model.py col896_conflicts)
+  const int k1 = t;
 #pragma unroll
   for (int tt = 0; tt < 32; ++tt) v[tt] = *sc.at(tt, k1);
   wave_sync();

@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
 
   const int grp = threadIdx.x / R;
   const int t = threadIdx.x % R;
-  const int lane_base = (threadIdx.x & 63) - t;
+  const int k1 = mirror_k1(t);         // r05: the second FFT stage in mirror-paired lane order
   constexpr int RB = N / GPB;
   constexpr int RBW = RB / RIT;
   int bid = RIT == 1 ? xcd_pair<RB>(blockIdx.x) : (int)blockIdx.x;
@@ -320,23 +320,24 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
       load_row(it + 1 < RIT ? y + GPB : y);
       if (it > 0) lds_barrier();   // every group has read the previous plane-b tile
     }
-    fft_group_split<R, false>(v, t, lds + grp * R * (R + 1), tw);
+    // lane t now holds Z[k1 + 32 k2] (k1 = mirror_k1(t)): the mirror partner is lane t ^ 1
+    fft_group_split_mirror<false>(v, t, k1, lds + grp * R * (R + 1), tw);
 
     // Hermitian split: plane a now, plane b kept in registers for the second tile
     float2 fb[R / 2];
     lds_barrier();    // every group is done with its FFT tile: reuse as the plane tile
-    const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0
+    const float2 zny = from_pk(v[R / 2]);  // Z[N/2] on lane 0 (k1 = 0)
 #pragma unroll
     for (int k2 = 0; k2 < R / 2; ++k2) {
       const float2 z = from_pk(v[k2]);
-      const float2 m = mirror_conj<R>(v, k2, t, lane_base);
+      const float2 m = mirror_conj_paired(v, k2, t);
       float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
       fb[k2] = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
       if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
         fa = make_float2(z.x, zny.x);
         fb[k2] = make_float2(z.y, zny.y);
       }
-      tile[tile_pos<R, GPB>(t + R * k2, grp)] = fa;
+      tile[tile_pos<R, GPB>(k1 + R * k2, grp)] = fa;
     }
     constexpr int CHUNKS = (N / 2) * GPB / 2;   // 16-B chunks of one plane's panel
     static_assert(CHUNKS % NT == 0, "chunking");
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
       if (pl == 1) {
         lds_barrier();   // plane a's tile has been read
 #pragma unroll
-        for (int k2 = 0; k2 < R / 2; ++k2) tile[tile_pos<R, GPB>(t + R * k2, grp)] = fb[k2];
+        for (int k2 = 0; k2 < R / 2; ++k2) tile[tile_pos<R, GPB>(k1 + R * k2, grp)] = fb[k2];
       }
       lds_barrier();
 #pragma unroll

@@ -186,9 +186,14 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
         const int c = threadIdx.x + 256 * i;
         const int r2 = (c % (kGPB / 2)) * 2;
         const int line = c / (kGPB / 2);
-        const float2 a = tile[tile896_pos(line, r2)];
-        const float2 b = tile[tile896_pos(line, r2 + 1)];
-        st_stream4(panel + 2 * c, make_float4(a.x, a.y, b.x, b.y));   // = a896_at(line, y0 + r2)
+        // rows r2, r2 + 1 of the line sit in one aligned 16-B pair (the XOR swizzle permutes whole
+        // pairs; its bit 0 swaps the two halves): one ds_read_b128, whose 16-lane groups cover
+        // four whole lines -- conflict-free for any swizzle inside a line (r05; two ds_read_b64
+        // cost 16 extra LDS cycles per 56 reads, 1.8 M per 128-job launch)
+        const int p0 = tile896_pos(line, r2);
+        const float4 ab = *reinterpret_cast<const float4*>(tile + (p0 & ~1));
+        const bool sw = (p0 & 1) != 0;
+        st_stream4(panel + 2 * c, sw ? make_float4(ab.z, ab.w, ab.x, ab.y) : ab);   // = a896_at(line, y0 + r2)
       }
     }
   }
@@ -248,8 +253,10 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
   const PaddedScratch<kR> sc{hs};
   const int k1 = t < kL ? t : 0;   // slot lane (28..31 carry don't-care values)
   // the mirror of ky = k1 + 28 k2 (k2 > 16) is 896 - ky = (28 - k1) + 28 (31 - k2), lane 0:
-  // 28 (32 - k2); the group wrote its ky <= 448 values as hs[k2 * 32 + lane]
-  const float2* hm = hs + ((t > 0 && t < kL) ? kL - t : kR);
+  // 28 (32 - k2); the group writes its ky <= 448 values as hs[k2 * 28 + lane] (lanes < 28; r05:
+  // rows of 28, not 32 -- with 32 lane 0's read hit lane 12's bank, 30 extra LDS cycles per wave
+  // and line; lanes 28..31 read don't-care values on the four banks no other lane uses)
+  const float2* hm = hs + (t == 0 ? kL : ((kL - t) & 31));
   // A line kx of a panel plane as seen by lane t: y = t + 32 jj -> a896_at(kx, t) + jj * 4 panels
   const int lane_a = (int)a896_at(0, t) * 8;
   constexpr int JSTEP = 4 * kHalf * kGPB * 8;   // bytes between registers jj and jj + 1
@@ -279,11 +286,13 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
     float2 w[32];
     if (!dc) {
       wave_sync();
+      if (t < kL) {
 #pragma unroll
-      for (int i = 0; i <= 16; ++i) hs[i * kR + t] = hb[i];
+        for (int i = 0; i <= 16; ++i) hs[i * kL + t] = hb[i];
+      }
       wave_sync();
 #pragma unroll
-      for (int i = 17; i < 32; ++i) hb[i] = hm[(31 - i) * kR];
+      for (int i = 17; i < 32; ++i) hb[i] = hm[(31 - i) * kL];
       wave_sync();
 #pragma unroll
       for (int i = 0; i < 32; ++i) {

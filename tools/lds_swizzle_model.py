@@ -165,7 +165,73 @@ def rowfwd896_tile_conflicts(pos):
     return wr, rd64, rd16
 
 
+def _wave(fn, rs=32 * 33):
+    """float2 addresses of one wave (two 32-lane groups, regions rs apart) -> dword addresses."""
+    out = []
+    for lane in range(64):
+        grp, t = lane // 32, lane % 32
+        a = fn(t)
+        out.append(None if a is None else 2 * (grp * rs + a))
+    return out
+
+
+def col896_conflicts(placement, b64_reads=0):
+    """Extra LDS cycles per wave and line iteration of k_col896 (hbx_passes896.hip) from the two
+    accesses with lane-dependent columns: fft896_ns_s2's transposed reads A'[tt][k1] (32 per
+    transpose; the compiler emits ds_read2_b64 -- two 16-lane / 32-bank accesses -- for all but
+    `b64_reads` of them, which go out as 32-lane / 64-bank ds_read_b64) and the H mirror's 15 reads.
+    placement "r04": lanes 28..31 read column 0, H rows of 32; "r05": lanes 28..31 read columns
+    28..31, H rows of 28 with lanes 28..31 on the four free banks."""
+    G16 = [range(i * 16, (i + 1) * 16) for i in range(4)]
+    G32 = [range(0, 32), range(32, 64)]
+    if placement == "r04":
+        k1 = lambda t: t if t < 28 else 0                                  # noqa: E731
+        hm = lambda i, t: (31 - i) * 32 + ((28 - t) if 0 < t < 28 else 32)  # noqa: E731
+    else:
+        k1 = lambda t: t                                                   # noqa: E731
+        hm = lambda i, t: (31 - i) * 28 + (28 if t == 0 else (28 - t) & 31)  # noqa: E731
+    tr = sorted((_extra(_wave(lambda t: tt * 33 + k1(t)), G16, 32), tt) for tt in range(32))
+    ex = sum(e for e, _ in tr[b64_reads:]) + sum(_extra(_wave(lambda t: tt * 33 + k1(t)), G32, 64)
+                                                  for _, tt in tr[:b64_reads])
+    ex += sum(_extra(_wave(lambda t: hm(i, t)), G16, 32) for i in range(17, 32))
+    # the writers: H rows (16-lane ds_write2_b64) must stay conflict-free as well
+    hw = (lambda i, t: i * 32 + t) if placement == "r04" else (lambda i, t: i * 28 + t if t < 28 else None)
+    ex += sum(_extra(_wave(lambda t: hw(i, t)), G16, 32) for i in range(17))
+    return ex
+
+
+MIRROR_K1 = [0, 16, 1, 31, 3, 29, 4, 28, 5, 27, 7, 25, 8, 24, 12, 20,
+             2, 30, 6, 26, 9, 23, 10, 22, 11, 21, 13, 19, 14, 18, 15, 17]   # hbx_fft.hpp kMirrorK1
+
+
+def rowfwd32_tile_write_conflicts(k1_of):
+    """Extra cycles of k_rowfwd32's lane-row plane-tile writes (tile_pos<32, 8> of line k1 + 32 k2,
+    row = the lane group; 16-lane / 32-bank service of ds_write_b64 / write2st64) per row block
+    and plane, for the lane -> k1 order `k1_of`."""
+    G16 = [range(i * 16, (i + 1) * 16) for i in range(4)]
+    ex = 0
+    for w in range(4):
+        for k2 in range(16):
+            addrs = []
+            for lane in range(64):
+                grp, t = w * 2 + lane // 32, lane % 32
+                addrs.append(2 * tile_pos_32_8(k1_of(t) + 32 * k2, grp))
+            ex += _extra(addrs, G16, 32)
+    return ex
+
+
+def mirror_pair_order_ok(order=MIRROR_K1):
+    """The r05 mirror-paired order: a permutation of 0..31, lanes 0 / 1 hold the self-mirrored
+    k1 = 0 / 16, lanes (2m, 2m + 1) hold k1 and 32 - k1 (the partner is lane t ^ 1)."""
+    if sorted(order) != list(range(32)) or order[:2] != [0, 16]:
+        return False
+    return all(order[2 * m] + order[2 * m + 1] == 32 for m in range(1, 16))
+
+
 if __name__ == "__main__":
+    print("k_rowfwd32 tile writes: natural order", rowfwd32_tile_write_conflicts(lambda t: t),
+          "mirror-paired", rowfwd32_tile_write_conflicts(lambda t: MIRROR_K1[t]), mirror_pair_order_ok())
+    print("k_col896 extra LDS cycles per wave and line: r04", col896_conflicts("r04"), "r05", col896_conflicts("r05"))
     print("k_rowfwd896 tile (write, read_b64, read2): tile_pos<32, 8>", rowfwd896_tile_conflicts(tile_pos_32_8),
           "tile896_pos", rowfwd896_tile_conflicts(tile896_pos))
     for R in (32, 16):
