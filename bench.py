@@ -500,15 +500,18 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
     gen = torch.Generator(device="cuda").manual_seed(seed)
     n_pix = mcfg.channels * mcfg.height * mcfg.width
     actions = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda", dtype=torch.int64)
+    # the VecEnv gets numpy actions, as SB3's rollout hands them over (on_policy_algorithm.py:
+    # actions.cpu().numpy() -> env.step); they go into the host-mapped action row
+    actions_h = actions.cpu().numpy()
     for k in range(warmup):
-        vec.step(actions[k])
+        vec.step(actions_h[k])
         pure.step_device(actions[k])
     torch.cuda.synchronize()
     t_obs, t_pure = [], []
     for _ in range(reps):
         t0 = time.perf_counter()
         for k in range(warmup, warmup + steps):
-            obs, rew, dones, infos = vec.step(actions[k])
+            obs, rew, dones, infos = vec.step(actions_h[k])
         torch.cuda.synchronize()
         t_obs.append(time.perf_counter() - t0)
         t0 = time.perf_counter()
@@ -531,6 +534,7 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
             "obs_overhead_frac": round(ms / bare_ms - 1.0, 4),
             "pure_device_step_ms": round(pure_ms, 4), "overhead_vs_pure_device_step": round(ms / pure_ms - 1.0, 4),
             "obs_format": obs_format, "obs_keys": list(obs.keys()), "obs_shapes": shapes, "obs_are_views": views,
+            "actions": "numpy int64 [B] per step (SB3's form), written into the host-mapped action row",
             "note": "HologramVecEnv.step (SB3 VecEnv surface, obs_format='torch', auto_reset on): all five "
                     "observation keys returned as views of device buffers the step kernels keep current "
                     "(state as int8, stepped pre-rollback recon_image), rewards / dones / error word written "
@@ -708,6 +712,7 @@ def vecenv_step_sharded(mcfg, B, steps, warmup, tsrc, psrc, every, dev, world):
     gen = torch.Generator(device="cuda").manual_seed(13 + 7919 * hd.env_rank_world()[0])
     n_pix = mcfg.channels * mcfg.height * mcfg.width
     actions = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda", dtype=torch.int64)
+    actions_h = actions.cpu().numpy()          # SB3's numpy actions (host-mapped action row)
     buf = torch.zeros((every, 2, B), dtype=torch.float64, pin_memory=True)
     hb = buf.numpy()
     got = [0]
@@ -715,7 +720,7 @@ def vecenv_step_sharded(mcfg, B, steps, warmup, tsrc, psrc, every, dev, world):
     def run(k0, k1):
         j = 0
         for k in range(k0, k1):
-            obs, rew, dones, infos = vec.step(actions[k])
+            obs, rew, dones, infos = vec.step(actions_h[k])
             hb[j, 0] = rew
             hb[j, 1] = dones
             j += 1

@@ -532,6 +532,7 @@ int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, co
     if (n_env < 0) return fail(HBX_ERR_INVALID, "n_env");
     const int n = env_ids ? n_ids : n_env;
     if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_ids");
+    if (p->pd.G == 1) return HBX_OK;   // (ABI v12) nothing is ever pending with one group
     HBX_HIP(hipSetDevice(p->device));
     HBX_HIP(hbx::launch_obs_settle(env_ids, n, e->intensity, e->recon, e->recon_pending, p->pd.G,
                                    (size_t)p->pd.N * p->pd.N, (hipStream_t)stream));
@@ -550,6 +551,14 @@ int hbx_env_obs_sync(hbx_plan_t p, const hbx_env_buffers_t* e, int32_t n_env, co
   if (n <= 0) return n == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "n_ids");
   HBX_HIP(hipSetDevice(p->device));
   const PlanDev& pd = p->pd;
+  if (rc_on && pd.G == 1) {
+    // (ABI v12) one group: the step keeps no accepted-intensity cache, so the accepted state's
+    // intensity is re-propagated from the mask (the same kernels: the bits the steps compute)
+    if (!e->target) return fail(HBX_ERR_INVALID, "HBX_OBS_RECON needs env.target");
+    int rc2 = propagate_full(p, e->mask, e->target, env_ids, n, e->intensity, nullptr, nullptr, nullptr, nullptr,
+                             (hipStream_t)stream);
+    if (rc2) return rc2;
+  }
   HBX_HIP(hbx::launch_obs_sync(env_ids, n, e->mask, st_on ? e->state_bytes : nullptr, e->intensity,
                                rc_on ? e->recon : nullptr, e->recon_pending, (what & HBX_OBS_RESOLVE) ? 1 : 0,
                                pd.G * pd.P, pd.G,
@@ -678,6 +687,9 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   ep.reward_kind = prm->reward_kind;
   EnvDev base = env_dev(e);
   if (!base.error) base.error = p->err;   // the word k_jobs_from_actions sets
+  // (ABI v12) one colour group: every step rewrites recon whole, so nothing is ever restored from
+  // the intensity cache -- no pending reconcile, no copies (hbx.h, recon_pending)
+  if (to_recon && G == 1) base.recon_pending = nullptr;
   for (int b0 = 0; b0 < n_env; b0 += p->max_jobs) {
     const int n = std::min(p->max_jobs, n_env - b0);
     const EnvDev ed = env_offset(base, b0, CH, G, N);
@@ -688,12 +700,12 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
     }
     // the previous step's group: recon and intensity agree again before it is overwritten -- in
     // k_rowinv_d's epilogue at N = 1024 / 256 (no launch of its own), else k_recon_reconcile
-    const bool fuse_rc = to_recon && (pd.R == 32 || pd.R == 16);
+    const bool fuse_rc = to_recon && ed.recon_pending && (pd.R == 32 || pd.R == 16);
     pdx.rc_pending = fuse_rc ? ed.recon_pending : nullptr;
     pdx.rc_cache = fuse_rc ? e->intensity + (size_t)b0 * G * hw : nullptr;
     // N = 1024 / 256: the finalize kernel sums the row-block partials itself (no k_reduce_partials)
     pdx.skip_reduce = (pd.R == 32 || pd.R == 16) ? 1 : 0;
-    if (to_recon && !fuse_rc)
+    if (to_recon && ed.recon_pending && !fuse_rc)
       HBX_HIP(hbx::launch_recon_reconcile(ed.recon_pending, rec, e->intensity + (size_t)b0 * G * hw, n, G, hw, st));
     if (pdx.skip_reduce) {     // N = 1024 / 256: the first pass decodes the actions itself
       pdx.actions = actions + b0;

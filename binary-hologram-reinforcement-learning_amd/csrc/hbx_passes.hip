@@ -609,8 +609,15 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
         }
       }
     }
+    if (inten_by_env) {
+      // obs["recon_image"] (r05): streamed out non-temporal -- nothing on the device reads it
+      // before the next step rewrites it (the settle copy at G > 1 takes the accepted half)
 #pragma unroll
-    for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
+      for (int k = 0; k < R; ++k) __builtin_nontemporal_store(acc[k], orow + t + R * k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; ++k) orow[t + R * k] = acc[k];
+    }
   }
   // reduce over the R lanes of the group, fixed order -> bitwise reproducible
 #pragma unroll

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 11
+ABI_VERSION = 12
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1

@@ -239,6 +239,9 @@ class HologramVecEnv(_VecEnvBase):
         self.use_graph = bool(graph) and mode in ("fft", "planes")
         self._graph = None
         self._g_actions = None
+        self._graph_h = None          # the host-action fast path's graph (_graph_fast)
+        self._graph_h_key = None
+        self._graph_h_warm = False
         self.reward_kind = reward
         self.importance_samples = int(importance_samples) if reward == "importance" else 0
         self.importance_seed = int(importance_seed)
@@ -313,6 +316,10 @@ class HologramVecEnv(_VecEnvBase):
         self._h_rew = h[:8 * n].view(np.float64)
         self._h_term, self._h_trunc = h[17 * n:18 * n], h[18 * n:19 * n]
         self._h_err = h[self._row_bytes:self._row_bytes + 4].view(np.int32)
+        # host-mapped action row (r05): numpy actions -- what SB3 hands step() -- are written here
+        # and the first pass reads them straight from host memory (no H2D copy per step)
+        self._arow = HostRow(self.plan.lib, 8 * max(n, 1))
+        self._act_np = self._arow.array.view(np.int64)[:n]
         self._dev_index = self.device.index if self.device.type == "cuda" else None
         self._readback = torch.cuda.Event() if self.device.type == "cuda" else None
         self._actions = None
@@ -507,6 +514,42 @@ class HologramVecEnv(_VecEnvBase):
     def _fast_ok(self) -> bool:
         return self.mode != "psf" and not self.use_graph and self.action_format == "discrete"
 
+    def _host_actions(self, actions) -> bool:
+        """numpy / list actions of the discrete FFT-type step (SB3's DummyVecEnv hands step() a
+        numpy array): written into the host-mapped action row, which the step kernels read.
+        The previous step's kernels are done with the row (step() waited for them)."""
+        if self.mode == "psf" or self.action_format != "discrete" or isinstance(actions, torch.Tensor):
+            return False
+        a = np.asarray(actions)
+        if a.size != self.num_envs or a.dtype.kind not in "iub":
+            return False
+        self._act_np[:] = a.reshape(-1)
+        return True
+
+    def _graph_fast(self):
+        """The fast-path step (actions from the host-mapped row, results into the host-mapped
+        row) replayed from a HIP graph: one launch per step instead of the step's kernel
+        launches.  Recaptured when what the capture baked in changes (_graph_key).  Its own
+        graph: the device-tensor path (_graph_step) bakes in other pointers."""
+        key = self._graph_key()
+        if self._graph_h is not None and self._graph_h_key != key:
+            self._graph_h = None
+        if self._graph_h is None:
+            if not self._graph_h_warm:
+                # lazy plan buffers are allocated on the first step: run one eagerly
+                self._launch_fast(self._arow.device)
+                self._graph_h_warm = True
+                return
+            g = torch.cuda.CUDAGraph()
+            st = torch.cuda.Stream(device=self.device)
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.graph(g, stream=st):
+                self._launch_fast(self._arow.device)
+            torch.cuda.current_stream(self.device).wait_stream(st)
+            self._graph_h, self._graph_h_key = g, key
+        self._before_launch(STEP_OBS_KEYS)
+        self._graph_h.replay()
+
     def _launch_fast(self, actions_ptr: int):
         """hbx_env_step on the current stream with the results written into the host-mapped
         row; `actions_ptr` is any address the kernels can read B int64 actions from (a device
@@ -547,7 +590,12 @@ class HologramVecEnv(_VecEnvBase):
     def step(self, actions):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
         (done envs report their last observation as info["terminal_observation"])."""
-        if not self._fast_step(actions):
+        if self._host_actions(actions):
+            if self.use_graph and self.device.type == "cuda":
+                self._graph_fast()
+            else:
+                self._launch_fast(self._arow.device)
+        elif not self._fast_step(actions):
             self.step_device(actions)
             # the other paths write the device row: one device -> host copy (rewards, done flags,
             # the error word), queued behind the step
@@ -556,8 +604,8 @@ class HologramVecEnv(_VecEnvBase):
         # the observation views and infos are built while the step is in flight
         if self._readback is not None:
             self._readback.record()
-            if self.state.recon is not None and self.mode != "psf":
-                self._settle()
+            if self.state.recon is not None and self.mode != "psf" and self.cfg.groups > 1:
+                self._settle()                    # (ABI v12: nothing is pending at one group)
         obs = self.observe(stepped=True)
         infos = [{} for _ in range(self.num_envs)]
         if self._readback is not None:
@@ -748,8 +796,10 @@ class HologramVecEnv(_VecEnvBase):
         # every view of the host-mapped row goes before the memory does
         self._host_t = self._host_np = self._h_rew = self._h_term = self._h_trunc = self._h_err = None
         self._fast_args = None
-        self._graph = None
+        self._graph = self._graph_h = None
+        self._act_np = None
         self._hrow.close()
+        self._arow.close()
         self.plan.close()
 
 
@@ -863,10 +913,6 @@ class BinaryHologramEnv(spaces.EnvBase):
         self.num_pixels = self._vec.num_pixels
         c = self.cfg
         self._recon_shape = (1, c.groups, c.height, c.width)
-        # the action as the step kernels read it: host-mapped memory (hbx_host_alloc)
-        self._act_row = HostRow(self._vec.plan.lib, 8)
-        self._act = self._act_row.array.view(np.int64)
-        self._act_dev = None          # device copy, for the step paths that take a tensor (graph replay)
         self.host_syncs = 0           # blocking waits in step() (one per step)
         self.episode_num_count = 0
         self.initial_psnr = None
@@ -955,19 +1001,20 @@ class BinaryHologramEnv(spaces.EnvBase):
         """Queue the step of action `a`, the recon readback and the settle; wait once.
         Returns the stepped recon_image (a fresh array backed by pinned memory)."""
         vec = self._vec
-        if vec._fast_ok():
-            self._act[0] = a                      # the previous step's kernels finished (waited below)
-            vec._launch_fast(self._act_row.device)
-        else:                                     # graph replay / MultiDiscrete: the tensor path
-            if self._act_dev is None:
-                self._act_dev = torch.zeros(1, dtype=torch.int64, device=vec.device)
-            self._act_dev.fill_(a)
-            vec.step_device(self._act_dev if vec.action_format == "discrete" else self._md_action(a))
+        if vec.action_format == "discrete":
+            vec._act_np[0] = a                    # the previous step's kernels finished (waited below)
+            if vec.use_graph:
+                vec._graph_fast()
+            else:
+                vec._launch_fast(vec._arow.device)
+        else:                                     # MultiDiscrete actions: the tensor path
+            vec.step_device(self._md_action(a))
             vec._host_t.copy_(vec._out_raw, non_blocking=True)
         recon = torch.empty(self._recon_shape, dtype=torch.float32, pin_memory=True)
         recon.copy_(vec.state.recon[0:1], non_blocking=True)   # env.py:179, queued behind the step
         vec._readback.record()
-        vec._settle()
+        if self.cfg.groups > 1:
+            vec._settle()
         vec._readback.synchronize()
         self.host_syncs += 1
         if vec._h_err[0]:
@@ -1063,8 +1110,6 @@ class BinaryHologramEnv(spaces.EnvBase):
 
     def close(self):
         self._vec.close()
-        self._act = None
-        self._act_row.close()
 
 class BinaryHologramEnvGroup(BinaryHologramEnv):
     """Drop-in for env_group.py's ``BinaryHologramEnv`` (env_group.py:37-320):

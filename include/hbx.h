@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 11
+#define HBX_ABI_VERSION 12
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -120,7 +120,12 @@ typedef struct hbx_env_buffers {
                               recon -> intensity; -(g+1): rolled back,
                               intensity -> recon; 0: none).  With recon given,
                               env->intensity of the last stepped group is
-                              current only after that reconcile.             */
+                              current only after that reconcile.
+                              ABI v12: with ONE colour group (G = 1) every step
+                              rewrites recon whole and nothing is ever restored,
+                              so no reconcile runs: recon_pending stays 0 and
+                              env->intensity keeps the last reset's / sync's
+                              values (HBX_OBS_RECON re-propagates it).        */
   /* ABI v9: plane-cached FFT mode (N = 1024 / 256; both non-null, with
    * hbx_env_reset / hbx_field_refresh filling them).  A step changes ONE plane
    * of the touched group, and the FFT mode's re-propagation of the other plane
@@ -424,7 +429,9 @@ int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_en
  * nullable = all n_env) from the state they mirror:
  *   HBX_OBS_STATE  state_bytes <- the mask bits
  *   HBX_OBS_RECON  recon <- intensity, recon_pending <- 0; the intensity cache is
- *                  taken as authoritative (it was just rewritten: reset, checkpoint load)
+ *                  taken as authoritative (it was just rewritten: reset, checkpoint load).
+ *                  ABI v12, G = 1: intensity is first re-propagated from the mask (the
+ *                  step keeps no cache at one group; needs env->target)
  *   HBX_OBS_RESOLVE (ABI v10, with HBX_OBS_RECON) apply the last step's pending
  *                  reconcile first: after an accepted step the stepped group's new
  *                  intensity lives in recon only (recon_pending = group + 1), so that
@@ -437,6 +444,7 @@ int hbx_env_step_psf(hbx_plan_t plan, const hbx_env_buffers_t* env, const hbx_en
  *                  envs keep their pending restore for the next step.  A VecEnv queues
  *                  it right behind the step's readback, so the copy runs while the host
  *                  turns the step around instead of inside the next step's k_rowinv.
+ *                  ABI v12: a no-op at G = 1 (nothing is pending).
  * hbx_env_reset does both for the envs it resets; a caller that restores
  * masks or intensities by itself (checkpoint load) calls it after. */
 #define HBX_OBS_STATE 1

@@ -138,11 +138,14 @@ def test_obs_step_matches_oracle_small():
     env.close()
 
 
-@pytest.mark.parametrize("mode", ["fft", "planes"])
-def test_graph_replayed_step_equals_eager(mode):
+@pytest.mark.parametrize("mode,src", [("fft", "tensor"), ("planes", "tensor"), ("fft", "numpy"),
+                                      ("planes", "numpy")])
+def test_graph_replayed_step_equals_eager(mode, src):
     """HologramVecEnv(graph=True): the device step captured once into a HIP graph and replayed
     gives the eager step's rewards, flags, observations and state at every step, across
-    auto-resets of env subsets (which run eagerly between replays)."""
+    auto-resets of env subsets (which run eagerly between replays).  src="numpy": the graph env
+    gets numpy actions (what SB3 passes), read by the kernels from the host-mapped action row
+    (r05, its own graph), against the eager env's device-tensor actions."""
     import hbx
     from hbx.env import HologramVecEnv, OBS_KEYS
     cfg = hbx.mono_config(256)
@@ -157,19 +160,21 @@ def test_graph_replayed_step_equals_eager(mode):
     graph.reset()
     acts = torch.randint(0, cfg.channels * 256 * 256, (80, B), generator=g, device="cuda")
     n_done = 0
+    acts_h = acts.cpu().numpy()
     for k in range(80):
         o1, r1, d1, _ = eager.step(acts[k])
-        o2, r2, d2, _ = graph.step(acts[k])
+        o2, r2, d2, _ = graph.step(acts[k] if src == "tensor" else acts_h[k])
         assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
         for key in OBS_KEYS:
             assert torch.equal(o1[key], o2[key]), (k, key)
         n_done += int(d1.sum())
-    assert graph._graph is not None and n_done > 0
+    assert (graph._graph if src == "tensor" else graph._graph_h) is not None and n_done > 0
     for key in ("mask", "chan_stats", "prev_psnr", "steps", "flip_count"):
         assert torch.equal(getattr(eager.state, key), getattr(graph.state, key)), key
 
 
-def test_graph_step_follows_set_attr_and_plan_changes():
+@pytest.mark.parametrize("src", ["tensor", "numpy"])
+def test_graph_step_follows_set_attr_and_plan_changes(src):
     """a HIP graph keeps the kernel arguments it was captured with, and
     EnvParams go to k_env_step_finalize by value.  After set_attr('max_steps' / 'T_PSNR', ...)
     or a plan timing change the graph-replayed env must behave as the eager env does."""
@@ -187,10 +192,11 @@ def test_graph_step_follows_set_attr_and_plan_changes():
     eager.reset()
     graph.reset()
     acts = torch.randint(0, cfg.channels * 256 * 256, (60, B), generator=g, device="cuda")
+    acts_h = acts.cpu().numpy()
     ended = 0
     for k in range(60):
         if k == 5:                                      # after the graph has been captured
-            assert graph._graph is not None
+            assert (graph._graph if src == "tensor" else graph._graph_h) is not None
             for e in (eager, graph):
                 e.set_attr("max_steps", 12)
         if k == 30:
@@ -201,7 +207,7 @@ def test_graph_step_follows_set_attr_and_plan_changes():
         if k == 40:
             graph.plan.set_timing(64, 2)                # plan per-call state changes: recapture
         o1, r1, d1, i1 = eager.step(acts[k])
-        o2, r2, d2, i2 = graph.step(acts[k])
+        o2, r2, d2, i2 = graph.step(acts[k] if src == "tensor" else acts_h[k])
         assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
         assert [x.get("TimeLimit.truncated") for x in i1] == [x.get("TimeLimit.truncated") for x in i2], k
         assert [("terminal_observation" in x) for x in i1] == [("terminal_observation" in x) for x in i2], k
@@ -214,15 +220,19 @@ def test_graph_step_follows_set_attr_and_plan_changes():
     graph.close()
 
 
-def test_obs_sync_resolve_right_after_accepted_step():
+@pytest.mark.parametrize("G", [1, 3])
+def test_obs_sync_resolve_right_after_accepted_step(G):
     """hbx_env_obs_sync(HBX_OBS_RECON) right after an accepted step used to copy
     the stale intensity cache over the correct recon and drop the pending reconcile.  With
     HBX_OBS_RESOLVE (ABI v10) the pending group goes recon -> intensity first; afterwards recon and
     the intensity cache both equal the propagation of the accepted mask, pending is 0, and the env
-    keeps stepping exactly like an untouched twin."""
+    keeps stepping exactly like an untouched twin.  ABI v12: at one colour group nothing is ever
+    pending (every step rewrites recon whole) and HBX_OBS_RECON re-propagates the cache; the
+    RGB case keeps the pending reconcile."""
     import hbx
     from hbx import _lib
-    cfg = hbx.mono_config(256)
+    cfg = hbx.mono_config(256) if G == 1 else hbx.OpticsConfig(64, 64, 3, 2, (638e-9, 515e-9, 450e-9))
+    N = cfg.height
     B = 4
     env, g = _env(cfg, B, 77)
     twin, _ = _env(cfg, B, 77)
@@ -230,7 +240,7 @@ def test_obs_sync_resolve_right_after_accepted_step():
     twin.reset()
     st = env.state
     plan = hbx.Plan(cfg, max_jobs=B)
-    acts = torch.randint(0, cfg.channels * 256 * 256, (40, B), generator=g, device="cuda")
+    acts = torch.randint(0, cfg.channels * N * N, (40, B), generator=g, device="cuda")
     synced = 0
     for k in range(40):
         # step_device: VecEnv.step settles accepted steps itself (HBX_OBS_SETTLE), this test
@@ -243,7 +253,10 @@ def test_obs_sync_resolve_right_after_accepted_step():
         assert torch.equal(env.state.prev_psnr, twin.state.prev_psnr), k
         acc = env._acc.bool()
         if acc.any() and k % 3 == 0:
-            assert int(st.recon_pending[acc].min()) > 0
+            if G > 1:
+                assert int(st.recon_pending[acc].min()) > 0
+            else:
+                assert int(st.recon_pending.abs().sum()) == 0
             plan.env_obs_sync(st.bufs, B, _lib.OBS_RECON | _lib.OBS_RESOLVE)
             # recon now shows the CURRENT (accepted) state of every group, and so does the cache
             i_now, _, _ = plan.propagate(st.mask, st.target)
@@ -357,3 +370,61 @@ def test_step_chunked_batches_equal_one_batch():
         a.step(bad)
     a.close()
     b.close()
+
+
+def test_numpy_actions_use_the_host_row_and_equal_tensor_actions():
+    """SB3 hands VecEnv.step() numpy actions: they go into the host-mapped action row (no H2D copy;
+    ABI v11 host memory) and the step equals the device-tensor step, rewards / flags / observations,
+    including an out-of-range action raising like env.py's index error would."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.mono_config(256)
+    B = 5
+    g = torch.Generator(device="cuda").manual_seed(41)
+    pres = [torch.rand((cfg.channels, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=15, obs_keys=OBS_KEYS)
+    a = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    b = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    a.reset()
+    b.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (40, B), generator=g, device="cuda")
+    acts_h = acts.cpu().numpy()
+    for k in range(40):
+        o1, r1, d1, _ = a.step(acts[k])
+        o2, r2, d2, _ = b.step(acts_h[k])
+        assert np.array_equal(r1, r2) and np.array_equal(d1, d2), k
+        assert np.array_equal(b._act_np, acts_h[k])
+        for key in OBS_KEYS:
+            assert torch.equal(o1[key], o2[key]), (k, key)
+    bad = acts_h[0].copy()
+    bad[2] = cfg.channels * 256 * 256
+    with pytest.raises(ValueError):
+        b.step(bad)
+    a.close()
+    b.close()
+
+
+def test_dropin_graph_replay_equals_eager():
+    """hbx.env.BinaryHologramEnv(graph=True): the drop-in step replayed from the host-action graph
+    returns the eager drop-in env's rewards, flags and observations."""
+    import hbx
+    from hbx.env import BinaryHologramEnv
+    N = 256
+    rng = np.random.default_rng(5)
+    pre = rng.random((8, N, N), np.float32)
+    tgt = rng.random((1, N, N), np.float32)
+    envs = [BinaryHologramEnv(lambda t: torch.from_numpy(pre[None]).to(t.device), [(torch.from_numpy(tgt[None]), ["x"])],
+                              max_steps=30, config=hbx.mono_config(N), verbose=False, graph=gr) for gr in (False, True)]
+    for e in envs:
+        e.reset()
+    ended = False
+    for k, a in enumerate(rng.integers(0, 8 * N * N, 34).tolist()):
+        (o1, r1, t1, u1, _), (o2, r2, t2, u2, _) = (e.step(a) for e in envs)
+        assert (r1, t1, u1) == (r2, t2, u2), k
+        for key in o1:
+            assert np.array_equal(o1[key], o2[key]), (k, key)
+        ended |= t1 or u1
+    assert envs[1]._vec._graph_h is not None and ended
+    for e in envs:
+        e.close()

@@ -2,10 +2,17 @@
 
     python tools/obs_cost.py [N]
 
-(a) step_device, obs_keys=()     (b) step_device with every observation buffer kept
-(c) VecEnv.step (host copy of rewards / dones each step, views as observations)
+(a) step_device, obs_keys=()                     the pure device step (launches back to back)
+(b) step_device with every observation buffer kept (the recon / state-byte writes)
+(c) VecEnv.step, obs_keys=()                     + the per-step host round trip only
+(d) VecEnv.step, every observation               the SB3-facing step
+(e) (d) without the settle launch                (the reconcile moves into the next k_rowinv)
+(f) (d) with obs_format="lazy", nothing read     (snapshots of the step-mutable keys)
+(g) (d) with numpy actions (SB3's form: the host-mapped action row)
+(h) (g) replayed from the host-action HIP graph (graph=True)
 """
 import os
+import statistics
 import sys
 import time
 
@@ -25,14 +32,18 @@ steps = 40 if N == 1024 else 300
 ALL = ("state_record", "state", "pre_model", "recon_image", "target_image")
 
 
-def run(keys, full):
+def run(keys, full, settle=True, fmt="torch", host=False, graph=False):
     vec = HologramVecEnv(cfg, B, lambda i: tg[i], pre_model_source=lambda i: pm[i], obs_keys=keys,
-                         auto_reset=full, max_steps=10 ** 9, refresh_every=0, obs_format="torch")
+                         auto_reset=full, max_steps=10 ** 9, refresh_every=0, obs_format=fmt, graph=graph)
     vec.reset()
-    acts = torch.randint(0, cfg.channels * N * N, (3 * steps + 10, B), device=dev)
+    if not settle:
+        vec._settle = lambda: None
+    acts = torch.randint(0, cfg.channels * N * N, (5 * steps + 10, B), device=dev)
+    if host:
+        acts = acts.cpu().numpy()
     k = 0
-    best = 1e9
-    for rep in range(3):
+    ts = []
+    for rep in range(5):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -42,13 +53,16 @@ def run(keys, full):
                 vec.step_device(acts[k])
             k += 1
         torch.cuda.synchronize()
-        best = min(best, (time.perf_counter() - t0) / steps * 1e3)
+        ts.append((time.perf_counter() - t0) / steps * 1e3)
     vec.close()
-    return best
+    return statistics.median(ts)
 
 
-a = run((), False)
-b = run(ALL, False)
-c = run(ALL, True)
-print(f"N={N}: bare {a:.4f}  obs-buffers {b:.4f} (+{(b - a) / a * 100:.1f}%)  "
-      f"VecEnv.step {c:.4f} (+{(c - a) / a * 100:.1f}%) ms/step", flush=True)
+res = {"a pure device step": run((), False), "b + obs buffers": run(ALL, False),
+       "c VecEnv.step, no obs": run((), True), "d VecEnv.step, all obs": run(ALL, True),
+       "e d without settle": run(ALL, True, settle=False), "f d lazy, unread": run(ALL, True, fmt="lazy"),
+       "g d, numpy actions": run(ALL, True, host=True), "h g, graph replay": run(ALL, True, host=True, graph=True)}
+a = res["a pure device step"]
+print(f"N={N}, B={B}, median of 5 x {steps} steps (ms/step, vs a):")
+for k, v in res.items():
+    print(f"  {k:28s} {v:.4f}  {(v - a) / a * 100:+.1f}%", flush=True)
