@@ -67,6 +67,7 @@ struct hbx_plan {
   int* walk_counter = nullptr;     // fused walk step: arrival tickets [9] (zero between launches)
   int walk_split = 0;              // HBX_WALK_SPLIT=1: three-launch batches for every K
   int walk_persist = 0;            // HBX_WALK_PERSIST=1: one cooperative launch per walk call
+  int32_t* planes_ticket = nullptr;  // hbx_dbs_walk_planes: the fused decision's arrival counter
 };
 
 namespace {
@@ -246,6 +247,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->pd.psf_partial) (void)hipFree(p->pd.psf_partial);
   if (p->walk_partial) (void)hipFree(p->walk_partial);
   if (p->walk_counter) (void)hipFree(p->walk_counter);
+  if (p->planes_ticket) (void)hipFree(p->planes_ticket);
   if (p->pd.psf_order) (void)hipFree(p->pd.psf_order);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
@@ -941,19 +943,25 @@ int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, 
   pdx.plane_slot = plane_slot;
   pdx.plane_spares = n_spare_pairs;
   pdx.spare_base = 0;
-  pdx.skip_reduce = 1;                     // k_walk_planes reduces the row-block partials itself
+  pdx.skip_reduce = 1;                     // the decision reduces the row-block partials itself
   const int RB = pd.N / (256 / pd.R);
-  auto step = [&](int decide) {
-    return hbx::launch_walk_planes(walk, order, p->jobs, pd.partial, RB, K, decide, base_mask, base_chan_stats,
-                                   plane_slot, accept_pos, accept_psnr, accept_cap, pd.G, pd.P, pd.N, pd.N,
-                                   pixel_count(p), p->optics.rel_scale, p->optics.peak, st);
-  };
-  HBX_HIP(step(0));                        // this call's first batch of jobs, from the walk state
-  for (int b = 0; b < batches; ++b) {
+  if (!p->planes_ticket) {   // the fused decision's arrival counter (first call only; reset by its user)
+    if (hipMalloc(&p->planes_ticket, 64) != hipSuccess) return fail(HBX_ERR_NOMEM, "walk ticket");
+    if (hipMemset(p->planes_ticket, 0, 64) != hipSuccess) return fail(HBX_ERR_HIP, "walk ticket");
+  }
+  hbx::WalkPlanesArgs wa;
+  wa.w = walk; wa.order = order; wa.jobs = p->jobs; wa.partial = pd.partial; wa.mask = base_mask;
+  wa.base_stats = base_chan_stats; wa.plane_slot = plane_slot; wa.accept_pos = accept_pos;
+  wa.accept_psnr = accept_psnr; wa.accept_cap = accept_cap; wa.ticket = p->planes_ticket;
+  wa.RB = RB; wa.K = K; wa.G = pd.G; wa.P = pd.P; wa.H = pd.N; wa.W = pd.N;
+  wa.count = pixel_count(p); wa.rel_scale = p->optics.rel_scale; wa.peak = p->optics.peak;
+  // (r05) each batch's decision runs in the last-arriving k_rowinv_d workgroup of that batch
+  // (k_rowinv_d<R, true>): three launches per batch instead of four
+  pdx.walk_planes = &wa;
+  HBX_HIP(hbx::launch_walk_planes(wa, 0, st));   // this call's first batch of jobs, from the walk state
+  for (int b = 0; b < batches; ++b)
     HBX_HIP(hbx::run_jobs(pdx, p->jobs, K, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,
                           nullptr, st));
-    HBX_HIP(step(1));
-  }
   return HBX_OK;
 }
 

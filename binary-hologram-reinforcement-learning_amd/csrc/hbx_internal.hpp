@@ -129,6 +129,25 @@ struct PassTimer {
   }
 };
 
+// the FFT-mode plane-cache walk's decision (hbx_walk_planes.hpp): everything it reads and writes
+struct WalkPlanesArgs {
+  hbx_dbs_walk_t* w;
+  const int64_t* order;
+  JobDesc* jobs;
+  const double* partial;     // [K][RB][3] row-block partials of the batch just propagated
+  uint64_t* mask;
+  double* base_stats;
+  int32_t* plane_slot;
+  int64_t* accept_pos;
+  double* accept_psnr;
+  int64_t accept_cap;
+  int32_t* ticket;           // fused decision: arrival counter of the k_rowinv_d workgroups
+  int RB, K, G, P, H, W;
+  double count;
+  int rel_scale;
+  double peak;
+};
+
 struct PlanDev {
   int R;               // N = R * R; 0: N = 896 = 28 x 32 (generic path)
   int N, G, P;
@@ -166,6 +185,8 @@ struct PlanDev {
   const int32_t* rc_pending; // [env] nullable
   float* rc_cache;           // [env][G][N][N] the intensity cache
   int skip_reduce = 0;       // 1: leave the per-row-block partials (a caller reduces them itself)
+  const WalkPlanesArgs* walk_planes = nullptr;   // (r05) plane-cache walk batch: the last k_rowinv_d
+                                                 // workgroup decides (hbx_walk_planes.hpp)
   // env step at N = 1024 / 256: the first pass decodes the actions itself (no k_jobs_from_actions
   // launch) and one of its workgroups per job writes the JobDesc the later passes read
   const int64_t* actions = nullptr;
@@ -316,10 +337,7 @@ hipError_t launch_psnr(const double* chan_stats, int n, int G, double* psnr, dou
 hipError_t launch_recon_reconcile(const int32_t* pending, float* recon, float* intensity, int n, int G,
                                   size_t hw, hipStream_t st);
 // plane cache (ABI v9): slot[env][i] = i for the listed envs (env_ids nullable: 0 .. n_ids - 1)
-hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* partial,
-                              int RB, int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
-                              int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int G, int P, int H,
-                              int W, double count, int rel, double peak, hipStream_t st);
+hipError_t launch_walk_planes(const WalkPlanesArgs& a, int decide, hipStream_t st);
 hipError_t launch_plane_slot_init(const int32_t* env_ids, int n_ids, int32_t* slot, int CHS, hipStream_t st);
 hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* mask, int8_t* state_bytes,
                            float* intensity, float* recon, int32_t* pending, int resolve, int CH, int G, size_t hw,

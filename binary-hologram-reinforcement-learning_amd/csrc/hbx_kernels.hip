@@ -9,6 +9,7 @@
 
 #include "hbx_fft.hpp"
 #include "hbx_internal.hpp"
+#include "hbx_walk_planes.hpp"
 
 namespace hbx {
 
@@ -391,175 +392,17 @@ __global__ void k_commit_flip(uint64_t* __restrict__ mask, double* __restrict__ 
 }
 
 // Device-decided greedy DBS in the FFT mode with the base state's plane cache (ABI v10,
-// hbx_dbs_walk_planes): one block.  decide = 1: the candidates of the batch just propagated
-// (jobs[c] = order[pos + c], each propagated against the batch's base state) are visited in order
-// by one thread, exactly as the serial loop (DBS_1024_24.py:313-363) visits them: a candidate's
-// PSNR is formed from its group's propagated stats and the CURRENT stats of the other groups
-// (k_eval_finalize's sum order), and the first strict improvement (:355) is committed as
-// hbx_commit_flip_planes does (mask bit, group stats, prev PSNR, the pair's spare slots swapped
-// in) and logged.  The visit then CONTINUES: a later candidate of a colour group no accept of
-// this batch has touched was propagated against exactly the group state the serial loop would
-// propagate it against (the other groups enter only through their stats), so its PSNR is the
-// serial loop's bit for bit; the batch ends before the first candidate of a touched group (it
-// needs a fresh propagation) -- up to G accepts per batch.  Then -- decide = 0 too -- the NEXT
-// batch's K jobs are written from the walk state (invalid jobs once the walk is done, so the
-// passes behind return at once).
-__device__ __forceinline__ double js_get(const double* js, int c, int i) { return js[3 * (size_t)c + i]; }
-
-__global__ void k_walk_planes(hbx_dbs_walk_t* __restrict__ w, const int64_t* __restrict__ order,
-                              JobDesc* __restrict__ jobs, const double* __restrict__ partial, int RB, int K,
-                              int decide, uint64_t* __restrict__ mask, double* __restrict__ base_stats,
-                              int32_t* __restrict__ plane_slot, int64_t* __restrict__ accept_pos,
-                              double* __restrict__ accept_psnr, int64_t accept_cap, int G, int P, int H, int W,
-                              double count, int rel_scale, double peak) {
-  // One block.  Everything the serial decision reads is fetched into LDS first, by many lanes and
-  // under the partial reduction: the walk state, the K jobs, the base statistics, each candidate's
-  // mask word and the two slot pairs its commit would swap, and the order window the next batch
-  // starts in (pos + [0, 2K)).  The decision itself (one lane, in candidate order) then runs on
-  // LDS and registers.  Measured: 11.7 us per launch against 11.0 for the r04j version that
-  // issued its global loads inside the loop (profiles/r04/walk_kernel_stats_r04{j,k}.txt) -- the
-  // launch is bound by its fixed chain (state -> order window / partials -> reduction ->
-  // decision -> job writes), not by the loop's loads.
-  constexpr int CJ = 8;                     // jobs per staging round of the partials
-  __shared__ double s_part[CJ * 3 * 128];   // RB <= 128 row blocks
-  __shared__ double s_js[256 * 3];
-  __shared__ JobDesc s_job[256];
-  __shared__ uint64_t s_word[256];          // candidate c's mask word
-  __shared__ int32_t s_slot[256][4];        // plane_slot[pa], [pa + 1], [CH + 2c], [CH + 2c + 1]
-  __shared__ int64_t s_order[512];          // order[pos + i], i < 2K
-  __shared__ double s_base[3 * HBX_MAX_GROUPS];
-  __shared__ int64_t s_pos, s_total, s_acc;
-  __shared__ int s_done, s_stop_en;
-  __shared__ double s_prev, s_last, s_init, s_stop_diff;
-  const int k = threadIdx.x;
-  const int64_t hw = (int64_t)H * W;
-  const int CH = G * P;
-  if (k == 0) {
-    s_pos = w->pos; s_total = w->total; s_acc = w->accepted; s_done = w->done;
-    s_stop_en = w->stop_enabled; s_prev = w->prev_psnr; s_last = w->last_psnr;
-    s_init = w->init_psnr; s_stop_diff = w->stop_diff;
-  }
-  if (decide && k < K) {
-    const JobDesc jb = jobs[k];
-    s_job[k] = jb;
-    if (jb.env >= 0) {
-      const int ch = jb.group * P + jb.flip_plane;
-      s_word[k] = mask[(size_t)ch * H * (W / 64) + (size_t)(jb.flip_pix / W) * (W / 64) + (jb.flip_pix % W) / 64];
-      const int pa = jb.group * P + (jb.flip_plane & ~1);
-      s_slot[k][0] = plane_slot[pa];
-      s_slot[k][1] = plane_slot[pa + 1];
-      s_slot[k][2] = plane_slot[CH + 2 * k];
-      s_slot[k][3] = plane_slot[CH + 2 * k + 1];
-    }
-  }
-  if (decide && k < 3 * G) s_base[k] = base_stats[k];
-  __syncthreads();                          // s_pos
-  {
-    const int64_t p0 = s_pos;
-    for (int i = k; i < 2 * K; i += blockDim.x) s_order[i] = (p0 + i < s_total) ? order[p0 + i] : -1;
-  }
-  if (decide) {
-    // k_reduce_partials fused (one launch per batch less): each candidate's three statistics
-    // summed over its row blocks in row-block order, k_reduce_partials' order bit for bit
-    for (int c0 = 0; c0 < K; c0 += CJ) {
-      const int nj = K - c0 < CJ ? K - c0 : CJ;
-      for (int i = k; i < nj * RB * 3; i += blockDim.x) s_part[i] = partial[(size_t)c0 * RB * 3 + i];
-      __syncthreads();
-      if (k < nj * 3) {
-        const int c = k / 3, st = k % 3;
-        double acc = 0.0;
-        for (int i = st; i < 3 * RB; i += 3) acc += s_part[c * 3 * RB + i];
-        s_js[3 * (c0 + c) + st] = acc;
-      }
-      __syncthreads();
-    }
-  }
-  __syncthreads();
-  if (k == 0 && decide && !s_done) {
-    const int64_t pos = s_pos;
-    const int nk = (int)min((int64_t)K, s_total - pos);
-    double prev = s_prev, last = s_last;
-    int64_t a = s_acc;
-    unsigned touched = 0;
-    int visited = nk, done = 0;
-    for (int c = 0; c < nk; ++c) {
-      const JobDesc jb = s_job[c];
-      if (jb.env >= 0 && ((touched >> jb.group) & 1u)) { visited = c; break; }
-      double ps = NAN;
-      const double* js = s_js + 3 * c;
-      if (jb.env >= 0) {
-        double sxy = 0.0, sxx = 0.0, syy = 0.0;
-        for (int gg = 0; gg < G; ++gg) {    // k_eval_finalize's sum order
-          if (gg == jb.group) { sxy += js[0]; sxx += js[1]; syy += js[2]; }
-          else { sxy += s_base[3 * gg]; sxx += s_base[3 * gg + 1]; syy += s_base[3 * gg + 2]; }
-        }
-        ps = psnr_from(sxy, sxx, syy, count, rel_scale, peak);
-      }
-      last = ps;
-      if (ps > prev) {                     // commit candidate c
-        const int ch = jb.group * P + jb.flip_plane;
-        const int pix = jb.flip_pix;
-        mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64] =
-            s_word[c] ^ (1ull << ((pix % W) & 63));
-        s_base[3 * jb.group] = js[0];
-        s_base[3 * jb.group + 1] = js[1];
-        s_base[3 * jb.group + 2] = js[2];
-        base_stats[3 * jb.group] = js[0];
-        base_stats[3 * jb.group + 1] = js[1];
-        base_stats[3 * jb.group + 2] = js[2];
-        const int pa = jb.group * P + (jb.flip_plane & ~1);
-        plane_slot[pa] = s_slot[c][2];        // the fresh pair's slots become current,
-        plane_slot[pa + 1] = s_slot[c][3];
-        plane_slot[CH + 2 * c] = s_slot[c][0];    // the replaced ones become spares
-        plane_slot[CH + 2 * c + 1] = s_slot[c][1];
-        if (a < accept_cap) { accept_pos[a] = pos + c; accept_psnr[a] = ps; }
-        ++a;
-        prev = ps;
-        touched |= 1u << jb.group;
-        if (s_stop_en && ps - s_init >= s_stop_diff) {   // DBS_ratio_0.5.py:366-372
-          done = 1;
-          w->stopped_early = 1;
-          visited = c + 1;
-          break;
-        }
-      }
-    }
-    w->accepted = a;
-    w->prev_psnr = prev;
-    w->last_psnr = last;
-    w->pos = pos + visited;
-    w->batches += 1;
-    const int d = (done || pos + visited >= s_total) ? 1 : 0;
-    if (d) w->done = 1;
-    s_done = d;
-    s_acc = visited;                         // reused: the next batch's offset in the order window
-  } else if (k == 0) {
-    s_acc = 0;
-  }
-  __syncthreads();
-  if (k < K) {                            // the next batch's jobs
-    const int off = (int)s_acc;
-    const int64_t q = s_pos + off + k;
-    JobDesc jd;
-    jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
-    if (!s_done && q < s_total) {
-      const int64_t av = s_order[off + k];
-      if (av >= 0 && av < (int64_t)G * P * hw) {
-        const int ch = (int)(av / hw);
-        jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(av % hw);
-      }
-    }
-    jobs[k] = jd;
-  }
+// hbx_dbs_walk_planes): the decision (hbx_walk_planes.hpp walk_planes_decide) in a launch of its
+// own -- each call's first batch of jobs (decide = 0).  Since r05 the per-batch decision runs in
+// the last-arriving workgroup of the batch's k_rowinv_d launch instead (one launch per batch less).
+__global__ void k_walk_planes(WalkPlanesArgs a, int decide) {
+  __shared__ __attribute__((aligned(16))) char lds[walk_planes_lds_bytes(128)];
+  walk_planes_decide<false>(a, decide, lds);
 }
 
-hipError_t launch_walk_planes(hbx_dbs_walk_t* w, const int64_t* order, JobDesc* jobs, const double* partial,
-                              int RB, int K, int decide, uint64_t* mask, double* base_stats, int32_t* plane_slot,
-                              int64_t* accept_pos, double* accept_psnr, int64_t accept_cap, int G, int P, int H,
-                              int W, double count, int rel, double peak, hipStream_t st) {
-  if (RB > 128 || K > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_walk_planes, dim3(1), dim3(256), 0, st, w, order, jobs, partial, RB, K, decide, mask,
-                     base_stats, plane_slot, accept_pos, accept_psnr, accept_cap, G, P, H, W, count, rel, peak);
+hipError_t launch_walk_planes(const WalkPlanesArgs& a, int decide, hipStream_t st) {
+  if (a.RB > 128 || a.K > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_walk_planes, dim3(1), dim3(256), 0, st, a, decide);
   return hipGetLastError();
 }
 

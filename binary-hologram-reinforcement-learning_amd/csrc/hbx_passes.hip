@@ -31,6 +31,7 @@
 #include "hbx_fft.hpp"
 #include "hbx_internal.hpp"
 #include "hbx_rowcol.hpp"
+#include "hbx_walk_planes.hpp"
 
 namespace hbx {
 
@@ -563,7 +564,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 // ---------------------------------------------------------------------------
 // k_rowinv's tail: plane mean, f64 partials of (I*T, I^2, T^2) against the target row,
 // fixed-order reduction over the group's lanes and the block's rows.
-template <int R, int GPB>
+template <int R, int GPB, bool SC1 = false>
 __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, const JobDesc& jb, int j, int y,
                                                 int rb, int grp, int t, const float* __restrict__ target,
                                                 size_t tmask, float* __restrict__ inten_out, int inten_by_env,
@@ -632,7 +633,14 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
     double a = 0.0, b = 0.0, cc = 0.0;
     for (int g = 0; g < GPB; ++g) { a += red[g][0]; b += red[g][1]; cc += red[g][2]; }
     double* o = partial + ((size_t)j * RB + rb) * 3;
-    o[0] = a; o[1] = b; o[2] = cc;
+    if constexpr (SC1) {   // read by the deciding workgroup of this launch (walk_planes_arrive)
+      const __amdgpu_buffer_rsrc_t ro = walk_planes_rsrc(o, 24);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), ro, 0, 0, kSc1Bit);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), ro, 8, 0, kSc1Bit);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, cc), ro, 16, 0, kSc1Bit);
+    } else {
+      o[0] = a; o[1] = b; o[2] = cc;
+    }
   }
 }
 
@@ -645,7 +653,7 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
 // plane's FFT is done (two blocks per CU cover them; a second register set for a plane in
 // flight took one block per CU and measured 1.80 ms against 1.47).  The r02
 // kernel staged every plane through an LDS tile between three block barriers (1.80 ms).
-template <int R>
+template <int R, bool WALK = false>
 __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__ jobs,
                                                      const float2* __restrict__ ws_b,
                                                      const float* __restrict__ target,
@@ -655,8 +663,9 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
                                                      int plane_mode, float* __restrict__ plane_pool,
                                                      const int32_t* __restrict__ plane_slot, int plane_spares,
                                                      int spare_base, const int32_t* __restrict__ rc_pending,
-                                                     float* __restrict__ rc_cache) {
+                                                     float* __restrict__ rc_cache, WalkPlanesArgs wk) {
   constexpr int N = R * R, GPB = 256 / R, RB = N / GPB, TL = 256 / R;
+  static_assert(!WALK || walk_planes_lds_bytes(RB) <= GPB * R * (R + 1) * 8, "the decision's LDS fits the scratch");
   __shared__ float2 tw[N];
   __shared__ float2 scratch[GPB * R * (R + 1)];
   __shared__ double red[GPB][3];
@@ -671,8 +680,14 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
   if (jb.env < 0) {
     if (threadIdx.x == 0) {
       double* o = partial + ((size_t)j * RB + rb) * 3;
-      o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
+      if constexpr (WALK) {
+        const __amdgpu_buffer_rsrc_t ro = walk_planes_rsrc(o, 24);
+        for (int i = 0; i < 3; ++i) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, ro, 8 * i, 0, kSc1Bit);
+      } else {
+        o[0] = 0.0; o[1] = 0.0; o[2] = 0.0;
+      }
     }
+    if constexpr (WALK) walk_planes_arrive(wk, reinterpret_cast<char*>(scratch));
     return;
   }
   const int y = rb * GPB + grp;
@@ -752,8 +767,12 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
     finish_plane(va, pa + 1);
 #pragma unroll 1
     for (int q = pa + 2; q < P; ++q) add_cached(q);
-    rowinv_epilogue<R, GPB>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial, red,
-                           rc_pending, rc_cache);
+    rowinv_epilogue<R, GPB, WALK>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env, partial,
+                                  red, rc_pending, rc_cache);
+    if constexpr (WALK) {
+      __syncthreads();   // every group is done with its scratch region: the decision's LDS
+      walk_planes_arrive(wk, reinterpret_cast<char*>(scratch));
+    }
     return;
   }
   load_plane(va, 0);
@@ -1062,11 +1081,22 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
   {
     const unsigned blocks = (unsigned)n_jobs * (N / (kRowNT<R> / R));
     if (tm) tm->begin(2, st);
-    if constexpr (kTiledB<R>)
-      hipLaunchKernelGGL(k_rowinv_d<R>, dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b, target ? target : pd.zero_row,
-                         pd.tw, P, pd.G, pd.partial, inten_out, field_out, target ? ~(size_t)0 : (size_t)0,
-                         pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot, pd.plane_spares,
-                         pd.spare_base, pd.rc_pending, pd.rc_cache);
+    if constexpr (kTiledB<R>) {
+      if (pd.walk_planes) {   // (r05) a plane-cache walk batch: the last workgroup decides
+        if (pd.plane_mode != kPlanesStep) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_rowinv_d<R, true>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
+                           target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                           target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,
+                           pd.plane_slot, pd.plane_spares, pd.spare_base, pd.rc_pending, pd.rc_cache,
+                           *pd.walk_planes);
+      } else {
+        hipLaunchKernelGGL((k_rowinv_d<R>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
+                           target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                           target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,
+                           pd.plane_slot, pd.plane_spares, pd.spare_base, pd.rc_pending, pd.rc_cache,
+                           WalkPlanesArgs{});
+      }
+    }
     else
       hipLaunchKernelGGL((k_rowinv<R, kRowNT<R>>), dim3(blocks), dim3(kRowNT<R>), 0, st, jobs, pd.ws_b,
                          target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out,

@@ -373,13 +373,20 @@ def planes_visited(q: float, k: int, groups: int) -> float:
     return vis
 
 
-def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0: float = 62.0,
-                  c: float = 15.0, fill: int = 2) -> int:
+# device-walk batch time (us) per speculation depth K at 1024 x 24, decision fused into the last
+# pass (r05, tools/dbs_walk_bench.py --k, profiles/r05/dbs_walk_k_r05o.txt; K = 1, 7 interpolated)
+_PLANES_BATCH_US = {1: 45.0, 2: 56.4, 3: 72.2, 4: 81.7, 5: 110.0, 6: 121.5, 7: 133.2, 8: 144.9}
+
+
+def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, table=None,
+                  slope: float = 11.7) -> int:
     """Speculation depth of the FFT-mode plane-cached walk for acceptance rate q: K minimising
-    the batch time / expected candidates visited (planes_visited), with the batch time t0 (us)
-    up to `fill` candidates and c us per candidate beyond.  Fit to the device walk's batches at
-    1024 x 24 (tools/dbs_walk_bench.py, profiles/r04/dbs_walk_k_r04f.txt: K = 2, 4, 6, 8 ->
-    62, 87, 127, 152 us per batch); at q = 0.5 it picks K = 3."""
+    the batch time / expected candidates visited (planes_visited).  Batch times from the measured
+    table (beyond it, `slope` us per candidate more); the step past K = 4 is the passes' workgroups
+    of K candidates no longer fitting the chip at once.  At q = 0.5 it picks K = 4 (34.0k
+    candidates/s against 33.3k at K = 3 on the r05 sweep)."""
+    tab = _PLANES_BATCH_US if table is None else table
+    kmax_t = max(tab)
     q = min(max(q, 1e-6), 1.0)
     # one pass of planes_visited's recursion gives the visited count of every k (the host runs
     # this once per 64-batch chunk: the per-k recomputation, O(k_max^2), took ~12 ms at k_max =
@@ -398,7 +405,8 @@ def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, t0
                     nxt[m + 1] += cont * q
         dist = nxt
         if k >= max(1, k_min):
-            cost = (t0 + c * max(0, k - fill)) / vis
+            t = tab[k] if k in tab else tab[kmax_t] + slope * (k - kmax_t)
+            cost = t / vis
             if cost < best:
                 best, bk = cost, k
     return bk

@@ -518,7 +518,12 @@ class HologramVecEnv(_VecEnvBase):
         """numpy / list actions of the discrete FFT-type step (SB3's DummyVecEnv hands step() a
         numpy array): written into the host-mapped action row, which the step kernels read.
         The previous step's kernels are done with the row (step() waited for them)."""
-        if self.mode == "psf" or self.action_format != "discrete" or isinstance(actions, torch.Tensor):
+        if self.mode == "psf" or self.action_format != "discrete":
+            return False
+        if type(actions) is np.ndarray and actions.dtype == np.int64 and actions.shape == self._act_np.shape:
+            np.copyto(self._act_np, actions)      # SB3's common case: no conversions on the critical path
+            return True
+        if isinstance(actions, torch.Tensor):
             return False
         a = np.asarray(actions)
         if a.size != self.num_envs or a.dtype.kind not in "iub":

@@ -37,7 +37,7 @@ def main():
         ("full_repropagation", dict(planes=False, device_walk=False)),
         ("planes_host", dict(planes=True, device_walk=False)),
         ("device_walk", dict())]
-    kw = {} if not a.k else {"k_max": a.k}
+    kw = {} if not a.k else {"k_min": a.k, "k_max": a.k}   # a fixed speculation depth
     for name, opts in variants:
         m = mask0.clone()
         dbs.greedy(plan, m.clone(), target, order[:512], **opts)       # warm-up
