@@ -234,8 +234,25 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
       const int c = threadIdx.x + NT * i;
       const int r2 = (c % (GPB / 2)) * 2;
       const int line = c / (GPB / 2);  // pl * N/2 + kx : A planes pa, pb are adjacent
-      const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
-      const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
+      float2 a, b;
+      if constexpr (GPB == 16) {
+        // (r05) rows r2, r2 + 1 sit in one aligned 16-B pair (the swizzle XORs whole pairs, its
+        // bit 0 swaps the halves): one ds_read_b128 from a single lane base (the swizzle keys on
+        // bits 0-4 of the line, which the chunk rounds i leave alone), conflict-free in the
+        // 4 x 16-lane model; the two ds_read_b64 it replaces were 2-way (0.79 M extra LDS cycles
+        // per 128-job launch at N = 256, profiles/r05/prof_mono_r05t); time unchanged (0.0587-0.0589
+        // vs 0.0587-0.0588 ms, profiles/r05/rowfwd16_ab_r05u.txt)
+        const int p0 = tile_pos<R, GPB>(line, r2);
+        const float4 ab = *reinterpret_cast<const float4*>(tile + (p0 & ~1));
+        const bool sw = (p0 & 1) != 0;
+        a = sw ? make_float2(ab.z, ab.w) : make_float2(ab.x, ab.y);
+        b = sw ? make_float2(ab.x, ab.y) : make_float2(ab.z, ab.w);
+      } else {
+        a = tile[tile_pos<R, GPB>(line, r2)];
+        b = tile[tile_pos<R, GPB>(line, r2 + 1)];
+      }
+      a = store_round<SK>(a);
+      b = store_round<SK>(b);
       const int pl = line / (N / 2);
       // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
       st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),

@@ -101,3 +101,19 @@ def test_rowfwd32_mirror_paired_order():
     body = hdr[hdr.index("kMirrorK1[32] = {"):]
     table = [int(v) for v in re.findall(r"\d+", body[body.index("{") + 1:body.index("}")])]
     assert table == M.MIRROR_K1
+
+
+def test_rowfwd16_b128_chunk_reads_conflict_free():
+    """r05 k_rowfwd<16, 256> (N = 256): each 16-B row pair of the 16-row plane tile is read with
+    one ds_read_b128 (the tile_pos<16, 16> swizzle XORs whole pairs) -- conflict-free, where the
+    r04 reads were 2-way: 128 extra cycles per workgroup and row block in the model if all 16 were
+    ds_read_b64 (the compiler emitted 12 of them plus two ds_read2st64_b64; the counter gave 0.79 M
+    per 128-job launch, profiles/r05/prof_mono_r05t -- the model does not reproduce that figure)."""
+    import lds_swizzle_model as M
+    assert M.rowfwd16_chunk_read_conflicts("b64") > 0
+    assert M.rowfwd16_chunk_read_conflicts("b128") == 0
+    # every chunk pair is one aligned 16-B pair of the tile (the b128 read's precondition)
+    for line in range(256):
+        for r2 in range(0, 16, 2):
+            p0, p1 = M.tile_pos_16(line, r2), M.tile_pos_16(line, r2 + 1)
+            assert p0 // 2 == p1 // 2 and p0 != p1

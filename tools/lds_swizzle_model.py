@@ -228,7 +228,47 @@ def mirror_pair_order_ok(order=MIRROR_K1):
     return all(order[2 * m] + order[2 * m + 1] == 32 for m in range(1, 16))
 
 
+def tile_pos_16(line, r):
+    """hbx_rowcol.hpp tile_pos<R, 16> (16-row tiles: the N = 256 k_rowfwd<16, 256>)."""
+    return line * 16 + (r ^ (((line & 15) ^ ((line >> 4) & 1)) & 15))
+
+
+B128_GROUPS = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)]]
+B128_GROUPS += [[lane + 32 for lane in g] for g in B128_GROUPS]
+
+
+def rowfwd16_chunk_read_conflicts(form, N=256, NT=256):
+    """Extra LDS cycles per workgroup and row block of k_rowfwd<16, 256>'s plane-tile chunk reads
+    (chunk c: line c / 8, rows r2 = 2 (c % 8) and r2 + 1): form "b64" = two ds_read_b64 (32-lane /
+    64-bank groups; r04), "b128" = one ds_read_b128 of the aligned 16-B pair (r05)."""
+    G32 = [range(0, 32), range(32, 64)]
+    ex = 0
+    for w in range(NT // 64):
+        for i in range(N * 16 // 2 // NT):
+            cs = [w * 64 + lane + NT * i for lane in range(64)]
+            if form == "b64":
+                for half in (0, 1):
+                    addrs = [2 * tile_pos_16(c // 8, (c % 8) * 2 + half) for c in cs]
+                    for g in G32:
+                        used = {}
+                        for lane in g:
+                            for d in (0, 1):
+                                used.setdefault((addrs[lane] + d) % 64, set()).add(addrs[lane] + d)
+                        ex += max(len(v) for v in used.values()) - 1
+            else:
+                base = [2 * (tile_pos_16(c // 8, (c % 8) * 2) & ~1) for c in cs]
+                for g in B128_GROUPS:
+                    used = {}
+                    for lane in g:
+                        for d in range(4):
+                            used.setdefault((base[lane] + d) % 64, set()).add(base[lane] + d)
+                    ex += max(len(v) for v in used.values()) - 1
+    return ex
+
+
 if __name__ == "__main__":
+    print("k_rowfwd<16> chunk reads: 2x ds_read_b64", rowfwd16_chunk_read_conflicts("b64"),
+          "ds_read_b128", rowfwd16_chunk_read_conflicts("b128"))
     print("k_rowfwd32 tile writes: natural order", rowfwd32_tile_write_conflicts(lambda t: t),
           "mirror-paired", rowfwd32_tile_write_conflicts(lambda t: MIRROR_K1[t]), mirror_pair_order_ok())
     print("k_col896 extra LDS cycles per wave and line: r04", col896_conflicts("r04"), "r05", col896_conflicts("r05"))
