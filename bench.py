@@ -265,6 +265,24 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
                              "accepted": sum(len(r.accepted_positions) for r in fres),
                              "note": "hbx.dbs.greedy_many(mode='fft'): one FFT-mode walk per image (own plan, "
                                      "plane cache and HIP stream), synthetic seeded images"}
+    # EXTENSION (BASELINE configs[4]'s "50 % on-pixel constraint"; no reference counterpart):
+    # the same prefix under the on-pixel ratio constraint (hbx_dbs_walk_planes_fill)
+    mfill = mask.clone()
+    dbs.greedy(plan, mfill.clone(), target, order[:256], fill_ratio=0.5, fill_tol=4)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rfill = dbs.greedy(plan, mfill, target, order, fill_ratio=0.5, fill_tol=4)
+    torch.cuda.synchronize()
+    dtfill = time.perf_counter() - t0
+    c0 = dbs.fill_counts(mask, cfg.groups, cfg.planes).tolist()
+    out["fill_ratio_extension"] = {
+        "flips": rfill.steps, "seconds": round(dtfill, 3), "flips_per_s": round(rfill.steps / dtfill, 1),
+        "accepted": len(rfill.accepted_positions), "psnr_gain_db": round(rfill.final_psnr - rfill.initial_psnr, 6),
+        "fill_ratio": 0.5, "fill_tol": 4, "group_counts_start": c0, "group_counts_end": rfill.fill_counts,
+        "target_count": dbs.fill_target(0.5, cfg.planes, N, N),
+        "note": "EXTENSION, no reference counterpart (SURVEY F7): greedy(fill_ratio=0.5) -- a candidate that "
+                "would move its colour group's on-pixel count away from 50 % by more than fill_tol pixels is "
+                "rejected without a propagation (hbx_dbs_walk_planes_fill); tests/test_gpu_fill.py"}
     out["full_repropagation"] = {
         "flips": rf.steps, "seconds": round(dtf, 3), "flips_per_s": round(rf.steps / dtf, 1),
         "same_accepts_and_psnr_bits_as_plane_cache": bool(

@@ -924,6 +924,16 @@ int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, 
                         float* plane_inten, int32_t* plane_slot, int32_t n_spare_pairs, const int64_t* order,
                         int64_t n_order, hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
                         int64_t accept_cap, int32_t K, int32_t batches, void* stream) {
+  return hbx_dbs_walk_planes_fill(p, base_mask, target, base_chan_stats, plane_inten, plane_slot, n_spare_pairs,
+                                  order, n_order, walk, accept_pos, accept_psnr, accept_cap, K, batches, nullptr,
+                                  0, 0, stream);
+}
+
+int hbx_dbs_walk_planes_fill(hbx_plan_t p, uint64_t* base_mask, const float* target, double* base_chan_stats,
+                             float* plane_inten, int32_t* plane_slot, int32_t n_spare_pairs, const int64_t* order,
+                             int64_t n_order, hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                             int64_t accept_cap, int32_t K, int32_t batches, int64_t* fill_count,
+                             int64_t fill_target, int64_t fill_tol, void* stream) {
   int rc = check_plan(p);
   if (rc) return rc;
   if (!base_mask || !target || !base_chan_stats || !plane_inten || !plane_slot || !order || !walk)
@@ -934,6 +944,9 @@ int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, 
   if (K < 1 || K > 256 || K > p->max_jobs || K > n_spare_pairs)
     return fail(HBX_ERR_INVALID, "K must be in [1, min(256, max_jobs, n_spare_pairs)]");
   if (batches < 0 || n_order < 0) return fail(HBX_ERR_INVALID, "batches / n_order");
+  if (fill_count && (fill_tol < 0 || fill_target < 0 ||
+                     fill_target > (int64_t)p->pd.P * p->pd.N * p->pd.N))
+    return fail(HBX_ERR_INVALID, "fill_target in [0, P*H*W] and fill_tol >= 0");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
   const PlanDev& pd = p->pd;
@@ -955,6 +968,7 @@ int hbx_dbs_walk_planes(hbx_plan_t p, uint64_t* base_mask, const float* target, 
   wa.accept_psnr = accept_psnr; wa.accept_cap = accept_cap; wa.ticket = p->planes_ticket;
   wa.RB = RB; wa.K = K; wa.G = pd.G; wa.P = pd.P; wa.H = pd.N; wa.W = pd.N;
   wa.count = pixel_count(p); wa.rel_scale = p->optics.rel_scale; wa.peak = p->optics.peak;
+  wa.fill_count = fill_count; wa.fill_target = fill_target; wa.fill_tol = fill_tol;
   // (r05) each batch's decision runs in the last-arriving k_rowinv_d workgroup of that batch
   // (k_rowinv_d<R, true>): three launches per batch instead of four
   pdx.walk_planes = &wa;

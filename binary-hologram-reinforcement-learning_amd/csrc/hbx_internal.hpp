@@ -146,6 +146,11 @@ struct WalkPlanesArgs {
   double count;
   int rel_scale;
   double peak;
+  // (ABI v13, extension) on-pixel ratio constraint: per-group on-pixel counts (nullptr = off),
+  // the target count and the tolerance (hbx_dbs_walk_planes_fill)
+  int64_t* fill_count = nullptr;
+  int64_t fill_target = 0;
+  int64_t fill_tol = 0;
 };
 
 struct PlanDev {

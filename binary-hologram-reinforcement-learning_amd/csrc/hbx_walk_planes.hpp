@@ -13,11 +13,24 @@ namespace hbx {
 
 constexpr int kWalkPlanesCJ = 8;             // jobs per staging round of the partials
 constexpr int kSc1Bit = 16;                  // buffer cache policy sc1 (gfx950): write-through / L2-fresh
+constexpr int kFillRejected = -2;            // job of a candidate the on-pixel constraint rejects (the
+                                             // passes skip every env < 0; the decision keeps its group)
 
 // LDS the decision needs for RB row blocks per job (carved out of a caller's buffer)
 __host__ __device__ constexpr size_t walk_planes_lds_bytes(int RB) {
   return (size_t)kWalkPlanesCJ * 3 * RB * 8 + 256 * 3 * 8 + 256 * sizeof(JobDesc) + 256 * 8 + 256 * 4 * 4 +
-         512 * 8 + 3 * HBX_MAX_GROUPS * 8 + 128;
+         512 * 8 + 3 * HBX_MAX_GROUPS * 8 + 128 + HBX_MAX_GROUPS * 8;
+}
+
+// (ABI v13, extension -- no reference counterpart) the on-pixel ratio constraint: a
+// flip moving group g's on-pixel count C by d = +-1 is admissible iff |C + d - T| <= tol or it
+// brings C closer to the target T.  hbx/dbs.py fill_admissible and oracle/hbx_oracle.py carry the
+// same rule.
+__host__ __device__ __forceinline__ bool fill_admissible(int64_t count, int64_t target, int64_t tol, int bit) {
+  const int64_t d = bit ? -1 : 1;
+  const int64_t now = count - target < 0 ? target - count : count - target;
+  const int64_t after = count + d - target < 0 ? target - count - d : count + d - target;
+  return after <= tol || after < now;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t walk_planes_rsrc(const void* base, unsigned bytes) {
@@ -59,6 +72,7 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
   int64_t* s_i64 = reinterpret_cast<int64_t*>(carve(3 * 8));           // pos, total, acc
   int* s_int = reinterpret_cast<int*>(carve(2 * 4));                    // done, stop_en
   double* s_dbl = reinterpret_cast<double*>(carve(4 * 8));              // prev, last, init, stop_diff
+  int64_t* s_fill = reinterpret_cast<int64_t*>(carve(HBX_MAX_GROUPS * 8));   // on-pixel counts (fill on)
   hbx_dbs_walk_t* w = a.w;
   const int k = threadIdx.x;
   const int64_t hw = (int64_t)H * W;
@@ -73,6 +87,7 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
   jb_k.env = -1;
   if (decide && k < K) jb_k = a.jobs[k];
   if (decide && k < 3 * G) s_base[k] = a.base_stats[k];
+  if (a.fill_count && k < G) s_fill[k] = a.fill_count[k];
   const __amdgpu_buffer_rsrc_t rp = walk_planes_rsrc(a.partial, (unsigned)((size_t)K * RB * 3 * 8));
   constexpr int PRE = 8;                    // partials per lane issued up front (first chunk)
   double pre[PRE];
@@ -155,7 +170,9 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
     int visited = nk, done = 0;
     for (int c = 0; c < nk; ++c) {
       const JobDesc jb = s_job[c];
-      if (jb.env >= 0 && ((touched >> jb.group) & 1u)) { visited = c; break; }
+      // (an inadmissible candidate, env == kFillRejected, was judged against the batch's starting
+      // count: it ends the batch like any other candidate of a touched group)
+      if (jb.env != -1 && ((touched >> jb.group) & 1u)) { visited = c; break; }
       double ps = NAN;
       const double* js = s_js + 3 * c;
       if (jb.env >= 0) {
@@ -183,6 +200,11 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
         a.plane_slot[pa + 1] = s_slot[4 * c + 3];
         a.plane_slot[CH + 2 * c] = s_slot[4 * c + 0];    // the replaced ones become spares
         a.plane_slot[CH + 2 * c + 1] = s_slot[4 * c + 1];
+        if (a.fill_count) {                  // the accepted flip's move of its group's on-pixel count
+          const int64_t f = s_fill[jb.group] + (((s_word[c] >> ((pix % W) & 63)) & 1ull) ? -1 : 1);
+          s_fill[jb.group] = f;
+          a.fill_count[jb.group] = f;
+        }
         if (acc_n < a.accept_cap) { a.accept_pos[acc_n] = pos + c; a.accept_psnr[acc_n] = ps; }
         ++acc_n;
         prev = ps;
@@ -218,6 +240,16 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
       if (av >= 0 && av < (int64_t)G * P * hw) {
         const int ch = (int)(av / hw);
         jd.env = 0; jd.group = ch / P; jd.flip_plane = ch % P; jd.flip_pix = (int)(av % hw);
+        if (a.fill_count) {
+          // an inadmissible candidate is visited and rejected without a propagation: a job the
+          // passes skip (no PSNR).  The counts are this decision's; an earlier accept of the next
+          // batch in the same group ends that batch at this candidate, which is then re-issued
+          // against the updated count
+          const int pix = jd.flip_pix;
+          const uint64_t word = a.mask[(size_t)ch * H * (W / 64) + (size_t)(pix / W) * (W / 64) + (pix % W) / 64];
+          if (!fill_admissible(s_fill[jd.group], a.fill_target, a.fill_tol, (int)((word >> ((pix % W) & 63)) & 1ull)))
+            jd.env = kFillRejected;
+        }
       }
     }
     a.jobs[k] = jd;

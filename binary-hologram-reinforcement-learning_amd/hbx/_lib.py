@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 12
+ABI_VERSION = 13
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
     "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
     "hbx_planes_fill", "hbx_eval_flips_planes", "hbx_commit_flip_planes", "hbx_dbs_walk_planes",
-    "hbx_host_alloc", "hbx_host_free",
+    "hbx_dbs_walk_planes_fill", "hbx_host_alloc", "hbx_host_free",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -133,6 +133,8 @@ def _declare(lib):
     lib.hbx_eval_flips_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I32, VP, VP, VP]
     lib.hbx_commit_flip_planes.argtypes = [VP, VP, VP, VP, VP, I32, VP, VP, VP, VP, I32, VP]
     lib.hbx_dbs_walk_planes.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I64, VP, VP, VP, I64, I32, I32, VP]
+    lib.hbx_dbs_walk_planes_fill.argtypes = [VP, VP, VP, VP, VP, VP, I32, VP, I64, VP, VP, VP, I64, I32, I32, VP,
+                                             I64, I64, VP]
     lib.hbx_host_alloc.argtypes = [C.c_size_t, C.POINTER(VP), C.POINTER(VP)]
     lib.hbx_host_free.argtypes = [VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]

@@ -46,6 +46,7 @@ class GreedyResult:
     accept_times: List[float] = field(default_factory=list)   # seconds since start, per accept
     last_psnr: Optional[float] = None    # psnr of the last visited candidate (accepted or not)
     seconds: float = 0.0
+    fill_counts: Optional[List[int]] = None   # on-pixel count per colour group at the end (fill_ratio runs)
 
 
 class KController:
@@ -61,6 +62,27 @@ class KController:
         else:
             self.k = int(min(self.k_max, max(self.k_min, 2 * (found_at + 1))))
         return self.k
+
+
+def fill_admissible(count: int, target: int, tol: int, bit: int) -> bool:
+    """The on-pixel ratio constraint (an EXTENSION: BASELINE configs[4] names a "50 % on-pixel
+    constraint", the reference has none -- SURVEY F7): flipping a pixel whose bit is `bit` moves
+    its colour group's on-pixel count by d = -1 / +1; admissible iff |count + d - target| <= tol or
+    the flip brings the count closer to the target (hbx_walk_planes.hpp fill_admissible)."""
+    d = -1 if bit else 1
+    after = abs(count + d - target)
+    return after <= tol or after < abs(count - target)
+
+
+def fill_counts(mask: torch.Tensor, groups: int, planes: int) -> np.ndarray:
+    """On-pixel count of each colour group of a packed mask [CH][H][W/64] int64 (host)."""
+    b = mask.detach().cpu().contiguous().numpy().view(np.uint8).reshape(groups, -1)
+    return np.unpackbits(b, axis=1).sum(axis=1).astype(np.int64)
+
+
+def fill_target(fill_ratio: float, planes: int, height: int, width: int) -> int:
+    """Target on-pixel count of one colour group (P planes of H x W)."""
+    return int(round(float(fill_ratio) * planes * height * width))
 
 
 def first_improving(psnr: np.ndarray, prev: float) -> Optional[int]:
@@ -414,9 +436,19 @@ def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, ta
 
 class _PlanesWalk(_Walk):
     """Host side of the device-decided FFT-mode walk (hbx_dbs_walk_planes): the same two
-    chunks in flight as _Walk, no refreshes (the FFT mode is exact), K from walk_k_planes."""
+    chunks in flight as _Walk, no refreshes (the FFT mode is exact), K from walk_k_planes.
+    fill = (fill_ratio, fill_tol): the on-pixel ratio constraint (hbx_dbs_walk_planes_fill)."""
+
+    def __init__(self, *args, fill=None, **kw):
+        self.fill = fill
+        super().__init__(*args, **kw)
 
     def _setup(self, plan, mask, target, total, stop_diff, k_min, k_max, refresh_every, dev, s):
+        self.fill_arg = None
+        if self.fill is not None:
+            c = plan.cfg
+            counts = torch.as_tensor(fill_counts(mask, c.groups, c.planes)).to(dev)
+            self.fill_arg = (counts, fill_target(self.fill[0], c.planes, c.height, c.width), int(self.fill[1]))
         self.k_hi = max(1, min(k_max, plan.max_jobs, 256))
         self.pool = plan.plane_pool(self.k_hi)
         stats, psnr0 = plan.planes_fill(mask, target, *self.pool, stream=s)
@@ -448,7 +480,13 @@ class _PlanesWalk(_Walk):
 
     def _chunk_n(self, stream, batches):
         self.plan.dbs_walk_planes(self.mask, self.target, self.base_stats, *self.pool, self.order_t, self.wbuf,
-                                  self.log_pos, self.log_psnr, self.k, batches, stream=stream)
+                                  self.log_pos, self.log_psnr, self.k, batches, stream=stream, fill=self.fill_arg)
+
+    def result(self) -> GreedyResult:
+        r = super().result()
+        if self.fill_arg is not None:
+            r.fill_counts = [int(v) for v in self.fill_arg[0].cpu().tolist()]
+        return r
 
     def advance(self):
         if self.finished:
@@ -562,7 +600,8 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
 def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_diff: Optional[float] = None,
            k_min: Optional[int] = None, k_max: Optional[int] = None, max_candidates: Optional[int] = None,
            stream=None, mode: str = "fft", refresh_every: int = 4096, progress=None,
-           graphs: bool = False, planes: Optional[bool] = None, device_walk: Optional[bool] = None) -> GreedyResult:
+           graphs: bool = False, planes: Optional[bool] = None, device_walk: Optional[bool] = None,
+           fill_ratio: Optional[float] = None, fill_tol: int = 1) -> GreedyResult:
     """mask [CH][H][W/64] int64 (modified in place), target [G][H][W] f32.
 
     mode="fft": every candidate is the FFT-mode propagation of its colour group
@@ -584,16 +623,28 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     from the running acceptance rate within [k_min (default 1), k_max]; host-decided batches
     (device_walk=False, mode="psf_host") grow K from k_min (default 4).  graphs=True replays the
     incremental walk's chunks from HIP graphs (mode="psf"); the FFT-mode device walk has no
-    graph variant and refuses it."""
+    graph variant and refuses it.
+    fill_ratio (EXTENSION, mode="fft" only; BASELINE configs[4]'s "50 % on-pixel constraint", which
+    the reference does not have -- SURVEY F7): a candidate whose flip would move its colour group's
+    on-pixel count away from round(fill_ratio * P * H * W) by more than fill_tol pixels is visited
+    and rejected without a propagation (fill_admissible); the result's fill_counts are the final
+    per-group counts.  Device walk: hbx_dbs_walk_planes_fill; host-decided batches: the same rule
+    on the host, so both give the same accept sequence."""
     if mode not in ("fft", "psf", "psf_host"):
         raise ValueError(f"mode must be 'fft', 'psf' or 'psf_host', got {mode!r}")
+    if fill_ratio is not None:
+        if mode != "fft":
+            raise ValueError("fill_ratio: the on-pixel constraint is built for mode='fft' only")
+        if not (0.0 <= float(fill_ratio) <= 1.0) or int(fill_tol) < 0:
+            raise ValueError("fill_ratio must be in [0, 1] and fill_tol >= 0")
     dev = plan.device
     if len(order) == 0 or max_candidates == 0:
         # nothing to visit: the serial loop's result over zero candidates (the device walks take
         # a non-empty order)
         _, _, p0 = plan.propagate(mask.unsqueeze(0), target.unsqueeze(0), want_intensity=False, stream=stream)
         init = float(p0.item())
-        return GreedyResult(init, init, 0, [], [], 0)
+        fc = None if fill_ratio is None else [int(v) for v in fill_counts(mask, plan.cfg.groups, plan.cfg.planes)]
+        return GreedyResult(init, init, 0, [], [], 0, fill_counts=fc)
     if mode == "psf":
         order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
         total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
@@ -616,7 +667,7 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
             raise ValueError("graphs=True: the FFT-mode device walk has no graph variant (device_walk=False "
                              "for host-decided batches, or mode='psf')")
         w = _PlanesWalk(plan, mask, target, order_t, total, stop_diff, k_min or 1, k_max, stream, 0,
-                        progress=progress)
+                        progress=progress, fill=None if fill_ratio is None else (fill_ratio, fill_tol))
         while not w.finished:
             w.advance()
         return w.result()
@@ -645,6 +696,14 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     acc_pos, acc_psnr, acc_t = [], [], []
     stopped = False
     last = None
+    fill = None
+    if fill_ratio is not None:           # host mirror of the bits and the per-group counts
+        c = plan.cfg
+        bits = np.unpackbits(mask.detach().cpu().contiguous().numpy().view(np.uint8),
+                             bitorder="little").reshape(c.channels, c.height, c.width)
+        fill = (bits, fill_counts(mask, c.groups, c.planes),
+                fill_target(fill_ratio, c.planes, c.height, c.width), int(fill_tol))
+        order_np = np.asarray(order, np.int64)
     t0 = time.perf_counter()
     while pos < total:
         k = min(ctl.k, total - pos)
@@ -659,13 +718,29 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
             plan.eval_flips(mask, target, base_stats, flips, psnr_buf[:k], gst_buf[:k], stream=stream)
         launches += 1
         ps = psnr_buf[:k].cpu().numpy()
+        if fill is not None:                 # inadmissible candidates: visited, rejected, no PSNR
+            bits, counts, f_t, f_tol = fill
+            c = plan.cfg
+            ps = ps.copy()
+            for j in range(k):
+                a = int(order_np[pos + j])
+                ch, rem = divmod(a, c.height * c.width)
+                r, col = divmod(rem, c.width)
+                if not fill_admissible(int(counts[ch // c.planes]), f_t, f_tol, int(bits[ch, r, col])):
+                    ps[j] = np.nan
         i = first_improving(ps, prev)
         ctl.update(i)
         if i is None:
-            last = float(ps[k - 1])
+            last = None if math.isnan(ps[k - 1]) else float(ps[k - 1])
             pos += k
             continue
         last = float(ps[i])
+        if fill is not None:
+            a = int(order_np[pos + i])
+            ch, rem = divmod(a, c.height * c.width)
+            r, col = divmod(rem, c.width)
+            fill[1][ch // c.planes] += -1 if bits[ch, r, col] else 1
+            bits[ch, r, col] ^= 1
         kdev.fill_(i)
         if mode == "psf":
             plan.commit_flip_psf(mask, base_stats, prev_dev, field, inten, flips, psnr_buf, gst_buf, kdev,
@@ -694,7 +769,8 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
             stopped = True
             break
     return GreedyResult(init, prev, pos, acc_pos, acc_psnr, launches, stopped, acc_t, last,
-                        time.perf_counter() - t0)
+                        time.perf_counter() - t0,
+                        fill_counts=None if fill is None else [int(v) for v in fill[1]])
 
 
 def greedy_report(res: GreedyResult, order, pre_model: np.ndarray, height: int, width: int,

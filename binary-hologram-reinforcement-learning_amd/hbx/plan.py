@@ -355,9 +355,11 @@ class Plan:
 
     def dbs_walk_planes(self, base_mask, target, base_stats, plane_inten, plane_slot, order: torch.Tensor,
                         walk: torch.Tensor, accept_pos: torch.Tensor, accept_psnr: torch.Tensor, K: int,
-                        batches: int, stream=None):
+                        batches: int, stream=None, fill=None):
         """hbx_dbs_walk_planes: enqueue `batches` device-decided batches of K candidates of the
-        FFT-mode greedy on the base state's plane pool (no host round trip)."""
+        FFT-mode greedy on the base state's plane pool (no host round trip).  fill = (counts, target,
+        tol): the on-pixel ratio constraint (hbx_dbs_walk_planes_fill, an extension; counts [G] int64
+        on the device, updated by the walk)."""
         c = self.cfg
         _need(base_mask, "base_mask", torch.int64, self.mask_shape(1)[1:], self.device)
         _need(target, "target", torch.float32, self.target_shape(1)[1:], self.device)
@@ -368,11 +370,21 @@ class Plan:
         cap = accept_pos.shape[0]
         _need(accept_pos, "accept_pos", torch.int64, (cap,), self.device)
         _need(accept_psnr, "accept_psnr", torch.float64, (cap,), self.device)
-        _lib.check(self.lib.hbx_dbs_walk_planes(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
-                                                _ptr(plane_inten), _ptr(plane_slot), s, _ptr(order),
-                                                int(order.shape[0]), _ptr(walk), _ptr(accept_pos),
-                                                _ptr(accept_psnr), cap, int(K), int(batches), _stream(stream)),
-                   "hbx_dbs_walk_planes")
+        if fill is None:
+            _lib.check(self.lib.hbx_dbs_walk_planes(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                                    _ptr(plane_inten), _ptr(plane_slot), s, _ptr(order),
+                                                    int(order.shape[0]), _ptr(walk), _ptr(accept_pos),
+                                                    _ptr(accept_psnr), cap, int(K), int(batches), _stream(stream)),
+                       "hbx_dbs_walk_planes")
+            return
+        counts, f_target, f_tol = fill
+        _need(counts, "fill counts", torch.int64, (c.groups,), self.device)
+        _lib.check(self.lib.hbx_dbs_walk_planes_fill(self._h, _ptr(base_mask), _ptr(target), _ptr(base_stats),
+                                                     _ptr(plane_inten), _ptr(plane_slot), s, _ptr(order),
+                                                     int(order.shape[0]), _ptr(walk), _ptr(accept_pos),
+                                                     _ptr(accept_psnr), cap, int(K), int(batches), _ptr(counts),
+                                                     int(f_target), int(f_tol), _stream(stream)),
+                   "hbx_dbs_walk_planes_fill")
 
     def eval_flips_psf(self, base_mask, target, base_stats, field, intensity, flips,
                        psnr_out=None, group_stats=None, stream=None):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 12
+#define HBX_ABI_VERSION 13
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -411,6 +411,21 @@ int hbx_dbs_walk_planes(hbx_plan_t plan, uint64_t* base_mask, const float* targe
                         int32_t n_spare_pairs, const int64_t* order, int64_t n_order,
                         hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
                         int64_t accept_cap, int32_t K, int32_t batches, void* stream);
+
+/* (ABI v13) EXTENSION, no reference counterpart (DBS_ratio_0.5.py has no on-pixel
+ * constraint; BASELINE configs[4] names one): hbx_dbs_walk_planes under an on-pixel ratio
+ * constraint.  fill_count[G] (device, caller-initialised) holds each colour group's on-pixel
+ * count over its P planes; a candidate that moves group g's count C by d = +1 (pixel 0 -> 1) or
+ * -1 is admissible iff |C + d - fill_target| <= fill_tol or |C + d - fill_target| < |C -
+ * fill_target|.  An inadmissible candidate is visited and rejected without a propagation (no
+ * PSNR); an accepted one updates fill_count.  fill_count NULL: hbx_dbs_walk_planes.  The
+ * host-decided batches of hbx.dbs.greedy(..., fill_ratio=) apply the same rule. */
+int hbx_dbs_walk_planes_fill(hbx_plan_t plan, uint64_t* base_mask, const float* target,
+                             double* base_chan_stats, float* plane_inten, int32_t* plane_slot,
+                             int32_t n_spare_pairs, const int64_t* order, int64_t n_order,
+                             hbx_dbs_walk_t* walk, int64_t* accept_pos, double* accept_psnr,
+                             int64_t accept_cap, int32_t K, int32_t batches, int64_t* fill_count,
+                             int64_t fill_target, int64_t fill_tol, void* stream);
 
 /* Incremental-field ("PSF") mode (reported separately from
  * the FFT-mode headline).  tt.simulate is linear, so flipping pixel (c, r, col)

@@ -442,18 +442,44 @@ def premodel_bin(value: float) -> int:
     return -1
 
 
-def dbs_greedy(env: OracleEnv, order: Sequence[int], stop_diff: Optional[float] = None):
+def fill_admissible(count: int, target: int, tol: int, bit: int) -> bool:
+    """EXTENSION (no reference counterpart -- SURVEY F7; BASELINE configs[4] names a "50 % on-pixel
+    constraint"): flipping a pixel whose bit is `bit` moves its colour group's on-pixel count by
+    -1 / +1; admissible iff the count ends within `tol` of `target` or closer to it than before."""
+    d = -1 if bit else 1
+    after = abs(count + d - target)
+    return after <= tol or after < abs(count - target)
+
+
+def group_fill_counts(state: np.ndarray, groups: int) -> np.ndarray:
+    """On-pixel count per colour group of an unpacked mask [CH][H][W]."""
+    return np.asarray(state, np.int64).reshape(groups, -1).sum(axis=1)
+
+
+def dbs_greedy(env: OracleEnv, order: Sequence[int], stop_diff: Optional[float] = None, fill=None):
     """Sequential greedy DBS (DBS.py:247-294, DBS_1024_24.py:313-422).
 
     Accept iff psnr_after > previous_psnr (strict).  Optional early stop once
     psnr - initial >= stop_diff (DBS_ratio_0.5.py:366-372, checked after every
-    candidate).  Returns (accepted flags, psnr per candidate, final psnr)."""
+    candidate).  fill = (target count, tol): the on-pixel ratio constraint (extension,
+    fill_admissible; an inadmissible candidate is rejected unevaluated, psnr NaN).
+    Returns (accepted flags, psnr per candidate, final psnr)."""
     accepted, psnrs = [], []
+    counts = None if fill is None else group_fill_counts(env.state, env.cfg.groups)
     for a in order:
+        if counts is not None:
+            ch, r, col = (int(v) for v in decode_action(a, env.cfg.height, env.cfg.width))
+            g = ch // env.cfg.planes
+            if not fill_admissible(int(counts[g]), fill[0], fill[1], int(env.state[ch, r, col])):
+                accepted.append(False)
+                psnrs.append(np.nan)
+                continue
         psnr_after, g, ig, st = env.evaluate_flip(int(a))
         ok = psnr_after > env.previous_psnr
         if ok:
             ch, r, col = (int(v) for v in decode_action(a, env.cfg.height, env.cfg.width))
+            if counts is not None:
+                counts[g] += -1 if env.state[ch, r, col] else 1
             env.state[ch, r, col] ^= 1
             env.intensity[g] = ig
             env.stats = st
@@ -538,16 +564,30 @@ class LinearGreedy:
         self.stats = st                                                   # :358-363
         self.previous_psnr = ev[0]
 
-    def run(self, order: Sequence[int], stop_diff: Optional[float] = None):
+    def run(self, order: Sequence[int], stop_diff: Optional[float] = None, fill=None):
         """Returns (accepted flags, psnr per candidate, psnr change per candidate
-        = psnr - previous psnr at that candidate) over ``order``."""
+        = psnr - previous psnr at that candidate) over ``order``.  fill = (target count, tol):
+        the on-pixel ratio constraint (extension, as dbs_greedy; rejected candidates: NaN)."""
         accepted, psnrs, deltas = [], [], []
+        c = self.cfg
+        self.fill_counts = None if fill is None else group_fill_counts(self.state, c.groups)
         for a in order:
+            if fill is not None:
+                ch, r, col = (int(v) for v in decode_action(a, c.height, c.width))
+                g = ch // c.planes
+                bit = int(self.state[ch, r, col])
+                if not fill_admissible(int(self.fill_counts[g]), fill[0], fill[1], bit):
+                    accepted.append(False)
+                    psnrs.append(np.nan)
+                    deltas.append(np.nan)
+                    continue
             ev = self.evaluate(int(a))
             ps = ev[0]
             ok = ps > self.previous_psnr                                   # :355 (strict)
             deltas.append(ps - self.previous_psnr)
             if ok:
+                if fill is not None:
+                    self.fill_counts[g] += -1 if bit else 1
                 self.commit(int(a), ev)
             accepted.append(ok)
             psnrs.append(ps)

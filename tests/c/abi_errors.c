@@ -70,6 +70,8 @@ int main(void) {
   CHECK(hbx_env_obs_sync(NULL, NULL, 0, NULL, 0, HBX_OBS_SETTLE, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_dbs_walk_planes(NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL) ==
         HBX_ERR_INVALID);
+  CHECK(hbx_dbs_walk_planes_fill(NULL, NULL, NULL, NULL, NULL, NULL, 1, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL, 0,
+                                 0, NULL) == HBX_ERR_INVALID);
   CHECK(hbx_dbs_walk_psf(NULL, NULL, NULL, NULL, NULL, NULL, NULL, 0, NULL, NULL, NULL, 0, 1, 1, NULL) ==
         HBX_ERR_INVALID);
   CHECK(hbx_plan_pipeline(NULL) == HBX_ERR_INVALID);

@@ -1,0 +1,116 @@
+"""The on-pixel ratio constraint on the FFT-mode greedy DBS -- an EXTENSION.
+
+BASELINE configs[4] reads "DBS_ratio_0.5: 1024x1024 with 50 % on-pixel constraint"; the reference
+has no such constraint (DBS_ratio_0.5.py stops at +0.5 dB, "ratio" names its
+pre-model histogram), so there is nothing of the reference's to match.  The rule (hbx.h
+hbx_dbs_walk_planes_fill, hbx.dbs.fill_admissible, oracle fill_admissible): a flip that moves
+its colour group's on-pixel count C by d = +-1 is admissible iff |C + d - T| <= tol or it
+brings C closer to T = round(ratio * P * H * W); an inadmissible candidate is visited and
+rejected without a propagation.
+
+Checked here: the device-decided walk (hbx_dbs_walk_planes_fill) and the host-decided batches
+make the same decisions with the same PSNR bits and end on the same mask and counts; both
+follow the float64 constrained serial loop (O.LinearGreedy.run(fill=...)) up to the first
+candidate whose change is within the f32 FFT resolution (as the unconstrained FFT-mode tests);
+the per-group deviation from T never grows past max(initial deviation, tol)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import hbx_oracle as O  # noqa: E402
+
+from tests.test_gpu_dbs_headline import FFT_TOL_DB, _dev, _first_difference, _fixture  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    import hbx
+    hbx.load_library()
+    yield
+
+
+def _runs(ocfg, pre, tgt, order, ratio, tol, **kw):
+    from hbx import dbs
+    out = []
+    for walk in (False, True):
+        plan, mask, target = _dev(ocfg, pre, tgt)
+        res = dbs.greedy(plan, mask, target, order, mode="fft", planes=True, device_walk=walk,
+                         fill_ratio=ratio, fill_tol=tol, **kw)
+        m = mask.cpu().numpy()
+        out.append((res, m, dbs.fill_counts(mask, ocfg.groups, ocfg.planes)))
+        plan.close()
+    return out
+
+
+def _check_same(runs):
+    (host, m_host, c_host), (walk, m_walk, c_walk) = runs
+    assert walk.accepted_positions == host.accepted_positions
+    assert walk.accepted_psnr == host.accepted_psnr                 # bit for bit
+    assert walk.steps == host.steps and walk.stopped_early == host.stopped_early
+    assert np.array_equal(m_host, m_walk)
+    assert walk.fill_counts == host.fill_counts == [int(v) for v in c_walk]
+
+
+@pytest.mark.parametrize("name,n_cand", [("dbs_prefix_1024x24_16k.npz", 2000), ("dbs_ratio05_256.npz", 3000)])
+def test_fill_walk_device_equals_host_and_oracle(golden_dir, name, n_cand):
+    """1024x24 (configs[4]'s size) at a 0.5 target -- the initial masks sit ~1e3 pixels off it,
+    so about half the candidates are inadmissible -- and 256x8 with the target AT the initial
+    count and tol 1, so the walk alternates around it."""
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, name)
+    order = order[:n_cand]
+    per_group = ocfg.planes * ocfg.height * ocfg.width
+    c0 = O.group_fill_counts((pre >= 0.5).astype(np.int8), ocfg.groups)
+    if ocfg.groups == 1:
+        ratio, tol = float(c0[0]) / per_group, 1
+    else:
+        ratio, tol = 0.5, 4
+    target = int(round(ratio * per_group))
+    runs = _runs(ocfg, pre, tgt, order, ratio, tol)
+    _check_same(runs)
+    walk = runs[1][0]
+    counts = np.asarray(walk.fill_counts)
+    dev0 = np.abs(c0 - target)
+    assert np.all(np.abs(counts - target) <= np.maximum(dev0, tol))
+    # the float64 constrained serial loop
+    lg = O.LinearGreedy(ocfg, pre, tgt)
+    acc, ps, delta = lg.run(order, fill=(target, tol))
+    rejected = np.isnan(ps)
+    print(f"{name}: {n_cand} candidates, {int(rejected.sum())} inadmissible, {int(acc.sum())} oracle accepts, "
+          f"{len(walk.accepted_positions)} device accepts, counts {c0.tolist()} -> {counts.tolist()} "
+          f"(target {target}, tol {tol})")
+    assert rejected.sum() > n_cand // 10 and acc.sum() > 20
+    first = _first_difference(walk.accepted_positions, acc)
+    if first is None:
+        assert np.array_equal(counts, lg.fill_counts)
+        assert abs(walk.final_psnr - lg.previous_psnr) <= 1e-4
+    else:
+        # a near-tie below the f32 FFT resolution (as test_fft_greedy_1024x24_vs_oracle)
+        assert not rejected[first] and abs(float(delta[first])) <= FFT_TOL_DB, (first, float(delta[first]))
+        assert first >= n_cand // 4
+
+
+def test_fill_walk_edges(golden_dir):
+    """tol 0 with the count on the target (every flip moves it away: all rejected, nothing
+    accepted), a ratio of 1.0 (only 0 -> 1 flips admissible), an early stop, and k_max 1."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_ratio05_256.npz")
+    per_group = ocfg.planes * ocfg.height * ocfg.width
+    c0 = int(O.group_fill_counts((pre >= 0.5).astype(np.int8), 1)[0])
+    o = order[:600]
+    runs = _runs(ocfg, pre, tgt, o, c0 / per_group, 0)
+    _check_same(runs)
+    assert runs[1][0].accepted_positions == [] and runs[1][0].fill_counts == [c0]
+    assert runs[1][0].steps == len(o)
+    runs = _runs(ocfg, pre, tgt, o, 1.0, 0)
+    _check_same(runs)
+    walk = runs[1][0]
+    bits = (pre >= 0.5).astype(np.int8)
+    c, r, col = O.decode_action(o[np.asarray(walk.accepted_positions, np.int64)], ocfg.height, ocfg.width)
+    assert len(walk.accepted_positions) > 10 and not bits[c, r, col].any()    # only 0 -> 1 flips
+    assert walk.fill_counts == [c0 + len(walk.accepted_positions)]
+    for kw in ({"stop_diff": 2e-3}, {"k_max": 1}):
+        _check_same(_runs(ocfg, pre, tgt, order[:1500], 0.5, 2, **kw))

@@ -265,6 +265,51 @@ def test_linear_greedy_equals_repropagating_oracle(field_kind):
     assert abs(lg.previous_psnr - final) <= 1e-12
 
 
+def test_fill_admissible_rule_and_host_copy_agree():
+    """The on-pixel ratio constraint (EXTENSION, BASELINE configs[4]; no reference counterpart,
+    SURVEY F7): within tol of the target, or closer to it.  hbx.dbs.fill_admissible (the host
+    decisions) and the oracle's are the same rule (the device's is hbx_walk_planes.hpp's)."""
+    from hbx.dbs import fill_admissible as host_rule
+    for count in range(0, 12):
+        for target in (4, 5, 6):
+            for tol in (0, 1, 2):
+                for bit in (0, 1):
+                    d = -1 if bit else 1
+                    want = abs(count + d - target) <= tol or abs(count + d - target) < abs(count - target)
+                    assert O.fill_admissible(count, target, tol, bit) == want == host_rule(count, target, tol, bit)
+
+
+@pytest.mark.parametrize("field_kind", [O.FIELD_AMPLITUDE, O.FIELD_PHASE])
+def test_fill_constrained_greedy_linear_equals_repropagating(field_kind):
+    """The constrained serial loop: LinearGreedy and the re-propagating dbs_greedy make the same
+    decisions, rejected candidates are NaN and were never accepted, and the per-group on-pixel
+    deviation from the target never grows past max(initial deviation, tol)."""
+    cfg = O.OpticsConfig(64, 64, 3, 2, O.WL_RGB, field_kind=field_kind)
+    pre, tgt = O.synthetic_inputs(cfg, 23)
+    env = O.OracleEnv(cfg, accept_rule=1)
+    env.reset(pre, tgt)
+    order = np.random.default_rng(5).permutation(cfg.channels * 64 * 64)[:500]
+    per_group = cfg.planes * 64 * 64
+    target, tol = per_group // 2, 1
+    dev0 = np.abs(O.group_fill_counts(env.state, cfg.groups) - target)
+    acc, ps, _ = O.dbs_greedy(env, order, fill=(target, tol))
+    lg = O.LinearGreedy(cfg, pre, tgt)
+    acc2, ps2, _ = lg.run(order, fill=(target, tol))
+    assert np.array_equal(acc, acc2)
+    assert np.array_equal(np.isnan(ps), np.isnan(ps2))
+    ok = ~np.isnan(ps)
+    assert np.max(np.abs(ps[ok] - ps2[ok])) <= 1e-12
+    assert np.isnan(ps).any() and not acc[np.isnan(ps)].any()
+    counts = O.group_fill_counts(env.state, cfg.groups)
+    assert np.array_equal(counts, lg.fill_counts)
+    assert np.all(np.abs(counts - target) <= np.maximum(dev0, tol))
+    # unconstrained, the same order accepts differently (the constraint binds)
+    env2 = O.OracleEnv(cfg, accept_rule=1)
+    env2.reset(pre, tgt)
+    acc3, _, _ = O.dbs_greedy(env2, order)
+    assert not np.array_equal(acc, acc3)
+
+
 @pytest.mark.parametrize("name,n_check", [("dbs_prefix_1024x24.npz", 12), ("dbs_ratio05_256.npz", 300)])
 def test_large_dbs_fixtures_reproduce(golden_dir, name, n_check):
     """The headline-size DBS fixtures (make_golden.py --large) against a fresh
