@@ -373,7 +373,7 @@ def dbs_prefix(cfg, mask, target, n_flips: int):
     return out
 
 
-def precision_sweep(mask1024, target1024, n_flips: int = 2048):
+def precision_sweep(mask1024, target1024, n_flips: int = 2048, n_constrained: int = 16384):
     """SURVEY 8d cfg 5 (BASELINE configs[4]): DBS_ratio_0.5.py's literal run -- 256x256x8
     mono greedy DBS until the PSNR has risen 0.5 dB (:366-372), FFT mode -- with f32 and
     with bf16-rounded pass intermediates (hbx_plan_set_precision), plus the per-flip PSNR
@@ -424,6 +424,34 @@ def precision_sweep(mask1024, target1024, n_flips: int = 2048):
         "flips": n_flips, "median_abs_change_db": float(np.median(np.abs(deltas["f32"]))),
         "bf16_rms_error_db": float(np.sqrt(np.mean(e * e))), "bf16_max_error_db": float(np.max(np.abs(e))),
         "bf16_sign_errors": float(np.mean(np.sign(deltas["bf16"]) != np.sign(deltas["f32"])))}
+    # configs[4]'s own wording: 1024 x 1024 under a 50 % on-pixel constraint (the EXTENSION of DESIGN
+    # 4k; the reference has no such constraint), fp32 vs bf16 intermediates over one candidate prefix
+    order24 = np.random.default_rng(3).permutation(24 * 1024 * 1024)[:n_constrained]
+    cons = {}
+    for name, prec in (("f32", PRECISION_F32), ("bf16", PRECISION_BF16_STORE)):
+        plan = Plan(cfg, max_jobs=256, precision=prec)
+        m = mask1024.clone()
+        t0 = time.perf_counter()
+        res = dbs.greedy(plan, m, target1024, order24, mode="fft", fill_ratio=0.5, fill_tol=4)
+        torch.cuda.synchronize()
+        cons[name] = (res, time.perf_counter() - t0)
+        plan.close()
+    (c32, ct32), (cbf, ctbf) = cons["f32"], cons["bf16"]
+    b32 = np.zeros(len(order24), bool)
+    bbf = np.zeros(len(order24), bool)
+    b32[c32.accepted_positions] = True
+    bbf[cbf.accepted_positions] = True
+    dd = np.nonzero(b32 != bbf)[0]
+    out["constrained_1024x24"] = {
+        "workload": f"1024x1024x24 FFT-mode greedy DBS over the first {len(order24)} candidates of rng(3), "
+                    "on-pixel ratio 0.5 +- 4 pixels per colour group (extension, DESIGN 4k)",
+        "f32": {"accepts": len(c32.accepted_positions), "psnr_gain_db": c32.final_psnr - c32.initial_psnr,
+                "final_fill_counts": c32.fill_counts, "seconds": round(ct32, 3)},
+        "bf16_intermediates": {"accepts": len(cbf.accepted_positions),
+                               "psnr_gain_db": cbf.final_psnr - cbf.initial_psnr,
+                               "final_fill_counts": cbf.fill_counts, "seconds": round(ctbf, 3)},
+        "final_psnr_deviation_db": abs(cbf.final_psnr - c32.final_psnr),
+        "first_accept_sequence_difference": int(dd[0]) if len(dd) else None}
     out["note"] = ("bf16 rounding of the stored intermediates (numerics only; layout and traffic stay f32). "
                    "The f32 path equals the float64 oracle's accept sequence on this run "
                    "(tests/test_gpu_dbs_headline.py::test_dbs_ratio05_256_literal_run)")
