@@ -553,7 +553,8 @@ def _walk_stream(device, i: int):
 def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: Sequence[torch.Tensor], orders,
                 stop_diff: Optional[float] = None, k_max: Optional[int] = None,
                 max_candidates: Optional[int] = None, refresh_every: int = 4096,
-                concurrency: int = 4, mode: str = "psf") -> List[GreedyResult]:
+                concurrency: int = 4, mode: str = "psf", fill_ratio: Optional[float] = None,
+                fill_tol: int = 1) -> List[GreedyResult]:
     """DBS_1024_24.py's loop over several images (`:208-211`), up to `concurrency`
     images' greedy walks side by side: walk i on plans[i] (one plan per image:
     its own workspace, tables and walk buffers) and its own HIP stream, the host
@@ -562,9 +563,12 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
     walks 191k).  mode "psf": the incremental-field walks (each result exactly
     greedy(mode="psf") on that image alone); "fft": the FFT-mode walks on the plane cache
     (hbx_dbs_walk_planes; each result exactly greedy(mode="fft") on that image alone).
-    Masks are modified in place."""
+    fill_ratio / fill_tol (mode="fft" only): the on-pixel ratio constraint of greedy() (an
+    extension, hbx_dbs_walk_planes_fill).  Masks are modified in place."""
     if mode not in ("psf", "fft"):
         raise ValueError(f"greedy_many: mode must be 'psf' or 'fft', got {mode!r}")
+    if fill_ratio is not None and mode != "fft":
+        raise ValueError("fill_ratio: the on-pixel constraint is built for mode='fft' only")
     if not (len(plans) == len(masks) == len(targets) == len(orders)):
         raise ValueError("one plan, mask, target and order per image")
     step = max(1, int(concurrency))
@@ -580,11 +584,13 @@ def greedy_many(plans: Sequence[Plan], masks: Sequence[torch.Tensor], targets: S
             order_t = torch.as_tensor(np.asarray(order, np.int64)).to(plan.device)
             total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
             if total == 0:                     # nothing to visit (the device walks take a non-empty order)
-                walks.append(greedy(plan, mask, target, [], mode="fft" if mode == "fft" else "psf"))
+                walks.append(greedy(plan, mask, target, [], mode="fft" if mode == "fft" else "psf",
+                                    fill_ratio=fill_ratio, fill_tol=fill_tol))
             elif mode == "fft":
                 km = min(k_max or plan.max_jobs, plan.max_jobs)
                 walks.append(_PlanesWalk(plan, mask, target, order_t, total, stop_diff, 1, km,
-                                         _walk_stream(plan.device, len(walks)), 0))
+                                         _walk_stream(plan.device, len(walks)), 0,
+                                         fill=None if fill_ratio is None else (fill_ratio, fill_tol)))
             else:
                 walks.append(_Walk(plan, mask, target, order_t, total, stop_diff, 1, k_max or _lib.WALK_MAX_K,
                                    _walk_stream(plan.device, len(walks)), refresh_every))

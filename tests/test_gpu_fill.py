@@ -114,3 +114,27 @@ def test_fill_walk_edges(golden_dir):
     assert walk.fill_counts == [c0 + len(walk.accepted_positions)]
     for kw in ({"stop_diff": 2e-3}, {"k_max": 1}):
         _check_same(_runs(ocfg, pre, tgt, order[:1500], 0.5, 2, **kw))
+
+
+def test_fill_greedy_many_equals_single_walks(golden_dir):
+    """greedy_many(mode="fft", fill_ratio=...): each image's constrained walk side by side equals
+    its single constrained greedy (accepts, PSNR bits, mask, counts)."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
+    rng = np.random.default_rng(9)
+    imgs = [(pre, tgt, order[:1500]), (rng.random(pre.shape).astype(pre.dtype), rng.random(tgt.shape).astype(tgt.dtype),
+                                       rng.permutation(order)[:1200])]
+    single = []
+    for p_, t_, o_ in imgs:
+        plan, mask, target = _dev(ocfg, p_, t_, max_jobs=16)
+        single.append((dbs.greedy(plan, mask, target, o_, mode="fft", fill_ratio=0.5, fill_tol=4), mask.cpu().numpy()))
+        plan.close()
+    devs = [_dev(ocfg, p_, t_, max_jobs=16) for p_, t_, _ in imgs]
+    many = dbs.greedy_many([x[0] for x in devs], [x[1] for x in devs], [x[2] for x in devs],
+                           [o_ for _, _, o_ in imgs], mode="fft", fill_ratio=0.5, fill_tol=4)
+    for (want, wm), got, (plan, gm, _) in zip(single, many, devs):
+        assert got.accepted_positions == want.accepted_positions
+        assert got.accepted_psnr == want.accepted_psnr
+        assert got.fill_counts == want.fill_counts
+        assert np.array_equal(gm.cpu().numpy(), wm)
+        plan.close()
