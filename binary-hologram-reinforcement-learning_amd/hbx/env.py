@@ -897,6 +897,11 @@ class BinaryHologramEnv(spaces.EnvBase):
                  device: Optional[int] = None, debug_timing: bool = False, **vec_kwargs):
         super().__init__()
         self.cfg = config or mono_config(256)
+        # (r05) the plane-cached FFT mode by default where it is built: every reward, PSNR, flag,
+        # mask and recon bit for bit the FFT mode's (tests/test_gpu_planes.py), one plane pair
+        # propagated per step -- 14.5k vs 13.9k steps/s at 256x8, 3.18k vs 2.97k at 1024x24 (B = 1,
+        # profiles/r05/dropin_modes_r05aj.txt).  mode="fft" re-propagates the whole group.
+        vec_kwargs.setdefault("mode", "planes" if self.cfg.height in (256, 1024) else "fft")
         if vec_kwargs.get("mode", "fft") == "psf":
             raise ValueError("BinaryHologramEnv returns the stepped recon_image (env.py:179): mode 'fft' or 'planes'")
         if "obs_keys" in vec_kwargs:

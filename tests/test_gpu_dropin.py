@@ -102,13 +102,16 @@ def _step_both(env, oe, a, clear_db):
 
 
 @pytest.mark.timeout(300)
-def test_dropin_env_256_mono_vs_oracle_with_max_steps_rollback():
+@pytest.mark.parametrize("mode", [None, "fft"])   # None: the default (plane-cached FFT mode at 256 / 1024)
+def test_dropin_env_256_mono_vs_oracle_with_max_steps_rollback(mode):
     from hbx.env import BinaryHologramEnv
     ocfg = O.mono_config(256)
     n_pix = ocfg.channels * 256 * 256
     loader, tf, ins = _setup(ocfg)
     max_steps = 200
-    env = BinaryHologramEnv(tf, loader, max_steps=max_steps, config=_dev_cfg(ocfg), verbose=False)
+    kw = {} if mode is None else {"mode": mode}
+    env = BinaryHologramEnv(tf, loader, max_steps=max_steps, config=_dev_cfg(ocfg), verbose=False, **kw)
+    assert env._vec.mode == (mode or "planes")
     obs, info = env.reset()
     pre, tgt = ins[0]
     assert info["state"] is obs["state"] is env.state                          # env.py:152,177 alias
