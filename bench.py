@@ -616,8 +616,9 @@ def dropin_env(N: int, G: int, steps: int, warmup: int):
         obs, reward, term, trunc, info = env.step(a)
     dt = time.perf_counter() - t0
     syncs = (env.host_syncs - s0) / steps
+    mode = env._vec.mode
     env.close()
-    return {"value": round(steps / dt, 2), "unit": "env-steps/s", "envs": 1, "steps": steps,
+    return {"value": round(steps / dt, 2), "unit": "env-steps/s", "envs": 1, "steps": steps, "mode": mode,
             "ms_per_step": round(dt / steps * 1e3, 4), "host_syncs_per_step": syncs,
             "obs": {k: [list(v.shape), str(v.dtype)] for k, v in obs.items()},
             "note": "hbx.env.BinaryHologramEnv.step (gymnasium contract, numpy obs dict): action into "
