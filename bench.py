@@ -568,11 +568,12 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
     dt = statistics.median(t_obs)
     pure_ms = statistics.median(t_pure) / steps * 1e3
     pure.close()
-    dev_obs = {k: obs.device(k) for k in obs.keys()} if obs_format == "lazy" else obs
-    shapes = {k: list(v.shape) for k, v in dev_obs.items()}
-    views = all(v.data_ptr() == getattr(vec.state, a).data_ptr() for k, v, a in
-                ((k, dev_obs[k], {"state_record": "record", "state": "state_bytes", "pre_model": "pre_model",
-                                  "recon_image": "recon", "target_image": "target"}[k]) for k in dev_obs))
+    shapes = {k: list(v.shape) for k, v in obs.items()} if obs_format == "torch" else \
+        {k: list(obs.device(k).shape) for k in obs.keys()}
+    views = obs_format == "torch" and all(v.data_ptr() == getattr(vec.state, a).data_ptr() for k, v, a in
+                                          ((k, obs[k], {"state_record": "record", "state": "state_bytes",
+                                                        "pre_model": "pre_model", "recon_image": "recon",
+                                                        "target_image": "target"}[k]) for k in obs))
     vec.close()
     ms = dt / steps * 1e3
     return {"value": round(B * steps / dt, 2), "unit": "env-steps/s", "envs": B, "steps": steps, "reps": reps,
@@ -588,6 +589,62 @@ def vecenv_step_obs(mcfg, B, steps, warmup, tsrc, psrc, bare_ms, seed, graph=Fal
                     "ppo_mono_256 line's device step (same measurement as the headline: sampled pass timing "
                     "and the per-8-step metric gather included); pure_device_step_ms is step_device of a twin "
                     "env without observations, timing or gather, alternated with the VecEnv runs"}
+
+
+def vecenv_step_obs_numpy(mcfg, B, steps, warmup, tsrc, psrc, seed, reps=2):
+    """The SB3-ingestible step: HologramVecEnv(obs_format="numpy") -- host
+    mirrors of state / state_record / pre_model / target_image updated by env.py:164-181's rules,
+    recon_image the one device -> host copy per step -- against r05's numpy path (every key
+    copied device -> host each step, emulated here as the torch-format step + .cpu().numpy() of
+    all five keys).  Each is timed bare and with every key read as SB3's DictRolloutBuffer.add
+    does (`observations[key][pos] = np.array(obs[key])`, buffers/rollout: one host copy per key
+    into a 2-row ring here); medians of `reps`."""
+    import statistics
+    import numpy as np
+    import torch
+    from hbx.env import OBS_KEYS, HologramVecEnv
+    kw = dict(pre_model_source=psrc, obs_keys=OBS_KEYS, auto_reset=True, max_steps=10 ** 9, T_PSNR=1e9,
+              T_PSNR_DIFF=1e9)
+    new = HologramVecEnv(mcfg, B, tsrc, obs_format="numpy", **kw)
+    old = HologramVecEnv(mcfg, B, tsrc, obs_format="torch", **kw)
+    o_new, o_old = new.reset(), old.reset()
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    n_pix = mcfg.channels * mcfg.height * mcfg.width
+    acts = torch.randint(0, n_pix, (warmup + steps, B), generator=gen, device="cuda").cpu().numpy()
+    ring = {k: np.empty((2,) + tuple(v.shape), v.dtype) for k, v in o_new.items()}
+
+    def run(env, to_np, add):
+        t0 = time.perf_counter()
+        for j, k in enumerate(range(warmup, warmup + steps)):
+            obs, _, _, _ = env.step(acts[k])
+            if to_np:
+                obs = {kk: v.cpu().numpy() for kk, v in obs.items()}
+            if add:
+                for kk in OBS_KEYS:
+                    ring[kk][j % 2] = np.array(obs[kk])
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    for k in range(warmup):
+        new.step(acts[k])
+        old.step(acts[k])
+    res = {"mirror": [], "mirror_add": [], "r05_numpy": [], "r05_numpy_add": []}
+    for _ in range(reps):
+        res["mirror"].append(run(new, False, False))
+        res["r05_numpy"].append(run(old, True, False))
+        res["mirror_add"].append(run(new, False, True))
+        res["r05_numpy_add"].append(run(old, True, True))
+    d2h = new._mirror.d2h_bytes
+    new.close()
+    old.close()
+    med = {k: round(statistics.median(v), 4) for k, v in res.items()}
+    return {"value": round(B / med["mirror"] * 1e3, 2), "unit": "env-steps/s", "envs": B, "steps": steps,
+            "reps": reps, "ms_per_step": med["mirror"], "ms_per_step_with_rollout_add": med["mirror_add"],
+            "r05_numpy_ms_per_step": med["r05_numpy"], "r05_numpy_ms_per_step_with_rollout_add": med["r05_numpy_add"],
+            "d2h_bytes_per_step": d2h,
+            "r05_d2h_bytes_per_step": int(sum(np.prod(v.shape) * v.itemsize for v in o_new.values())),
+            "note": "obs_format='numpy': only recon_image goes device -> host per step (d2h_bytes_per_step); "
+                    "r05_* is the torch-format step with every key copied device -> host, as r05's numpy "
+                    "format did; *_with_rollout_add also copies every key as SB3's DictRolloutBuffer.add"}
 
 
 def dropin_env(N: int, G: int, steps: int, warmup: int):
@@ -728,6 +785,56 @@ def shim_dbs_loop(N: int, flips: int, warmup: int):
             "note": "DBS.py:247-294's per-flip loop shape through torchOptics.optics.simulate / relativeLoss "
                     "(hbx_simulate underneath): full mask H2D, 8-plane propagation returning complex fields, "
                     "a host PSNR per flip -- the unchanged-caller path, not the device walk (dbs_greedy)"}
+
+
+def reset_cost(cfg, n_env: int = 8, reps: int = 5):
+    """Per-env HologramVecEnv.reset_envs time (env.py:90-152: threshold -> full propagation ->
+    initial PSNR) with the pre-model / target already on the device, for the mask packing as
+    shipped (hbx_pack_mask, one HIP launch, ABI v14) and as it was through r05 (torch ops:
+    `(pre >= 0.5)` -> int64 -> shift -> sum, several kernels materialising 8 B per pixel) --
+    the same reset otherwise, alternated, median of `reps`."""
+    import torch
+    import hbx.env as E
+    from hbx.env import HologramVecEnv
+    c = cfg
+    gen = torch.Generator(device="cuda").manual_seed(77)
+    pres = [torch.rand((c.channels, c.height, c.width), generator=gen, device="cuda") for _ in range(n_env)]
+    tgts = [torch.rand((c.groups, c.height, c.width), generator=gen, device="cuda") for _ in range(n_env)]
+    vec = HologramVecEnv(c, n_env, lambda i: tgts[i], pre_model_source=lambda i: pres[i], obs_keys=(),
+                         auto_reset=False)
+    shipped = E.pack_mask
+
+    def legacy(pre, threshold, out):
+        m = (pre >= threshold).to(torch.int64).reshape(*pre.shape[:-1], pre.shape[-1] // 64, 64)
+        shifts = torch.arange(64, device=pre.device, dtype=torch.int64)
+        out.copy_((m << shifts).sum(dim=-1, dtype=torch.int64))
+
+    def timed(fn):
+        E.pack_mask = fn
+        try:
+            vec.reset_envs(range(n_env))
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            vec.reset_envs(range(n_env))
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t0) / n_env * 1e3
+        finally:
+            E.pack_mask = shipped
+
+    timed(shipped)
+    new, old = [], []
+    mask_new = None
+    for _ in range(reps):
+        new.append(timed(shipped))
+        mask_new = vec.state.mask.clone()
+        old.append(timed(legacy))
+    same = bool(torch.equal(mask_new, vec.state.mask))
+    vec.close()
+    return {"ms_per_env": round(statistics.median(new), 4), "torch_pack_ms_per_env": round(statistics.median(old), 4),
+            "envs": n_env, "reps": reps, "masks_equal": same, "size": c.height, "planes": c.channels,
+            "note": "HologramVecEnv.reset_envs per env (pre-model and target resident on the GPU: threshold, full "
+                    "propagation of every group, initial PSNR); ms_per_env packs the mask with hbx_pack_mask (one "
+                    "HIP launch), torch_pack_ms_per_env with r05's torch ops -- alternated on the same env"}
 
 
 def check_devices(rows, world: int, rehearse: bool, dev) -> int:
@@ -1164,6 +1271,8 @@ def main():
                         obs_format="lazy").items() if k in ("value", "ms_per_step", "obs_overhead_frac",
                                                             "overhead_vs_pure_device_step")}
                     out["ppo_mono_256"]["vecenv_step_obs"] = vo
+                    out["ppo_mono_256"]["vecenv_step_obs_numpy"] = vecenv_step_obs_numpy(
+                        mono, B, 30, 5, mt, mp, 13)
             else:
                 vo = vecenv_step_sharded(mono, B, msteps, args.warmup, mt, mp, args.gather_every, dev, world)
                 if rank == 0:
@@ -1193,6 +1302,7 @@ def main():
                                       "vs_dropin": round(d["value"] / cb["value"], 1)}
         out["dropin_env_256"] = d
         out["dropin_env_1024x24"] = dropin_env(1024, 3, 60, 5)
+        out["reset_1024x24"] = reset_cost(cfg)
         torch.cuda.empty_cache()
 
     if rank == 0:

@@ -48,6 +48,8 @@ struct hbx_plan {
   int max_jobs;
   size_t ws_bytes;
   JobDesc* jobs;          // [max_jobs]
+  JobDesc* full_jobs;     // [max_jobs] (env i / G, group i % G): the jobs of every full propagation
+                          // without env ids, built once (ABI v14: one launch fewer per tt.simulate)
   float* job_inten;       // [max_jobs][N][N]
   int32_t* accept_flag;   // [max_jobs]
   int32_t* err;           // [1]
@@ -211,6 +213,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&pd.job_stats, (size_t)max_jobs * 3 * sizeof(double)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "job_stats");
   if (hipMalloc(&p->jobs, (size_t)max_jobs * sizeof(JobDesc)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "jobs");
+  if (hipMalloc(&p->full_jobs, (size_t)max_jobs * sizeof(JobDesc)) != hipSuccess)
+    return cleanup(HBX_ERR_NOMEM, "full jobs");
   if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "accept_flag");
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
@@ -223,7 +227,9 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMemcpy(pd.tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess ||
-      hipMemset(pd.zero_row, 0, (size_t)N * sizeof(float)) != hipSuccess)
+      hipMemset(pd.zero_row, 0, (size_t)N * sizeof(float)) != hipSuccess ||
+      hbx::launch_jobs_full(nullptr, max_jobs / G, G, p->full_jobs, nullptr) != hipSuccess ||
+      hipStreamSynchronize(nullptr) != hipSuccess)
     return cleanup(HBX_ERR_HIP, "table upload");
   *out = p;
   return HBX_OK;
@@ -239,6 +245,7 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->pd.partial) (void)hipFree(p->pd.partial);
   if (p->pd.job_stats) (void)hipFree(p->pd.job_stats);
   if (p->jobs) (void)hipFree(p->jobs);
+  if (p->full_jobs) (void)hipFree(p->full_jobs);
   if (p->job_inten) (void)hipFree(p->job_inten);
   if (p->accept_flag) (void)hipFree(p->accept_flag);
   if (p->err) (void)hipFree(p->err);
@@ -420,7 +427,9 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
     const int n = std::min(chunk, n_ids - i0);
     // with env_ids the jobs carry absolute env ids; without, ids are chunk-local
     // and every per-env buffer is offset by i0 instead
-    HBX_HIP(hbx::launch_jobs_full(env_ids ? env_ids + i0 : nullptr, n, G, p->jobs, st));
+    // with env ids the jobs are built per chunk; without, they are the plan's constant table
+    JobDesc* jobs = env_ids ? p->jobs : p->full_jobs;
+    if (env_ids) HBX_HIP(hbx::launch_jobs_full(env_ids + i0, n, G, jobs, st));
     const size_t mwords = (size_t)G * pd.P * pd.N * (pd.N / 64);
     const uint64_t* m = env_ids ? mask : mask + (size_t)i0 * mwords;
     const float* tg = (env_ids || !target) ? target : target + (size_t)i0 * G * pd.N * pd.N;
@@ -432,17 +441,18 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
       pdx.plane_pool = env_ids ? plane_pool : plane_pool + (size_t)i0 * CHs * pd.N * pd.N;
       pdx.plane_slot = env_ids ? plane_slot : plane_slot + (size_t)i0 * CHs;
     }
-    HBX_HIP(hbx::run_jobs(pdx, p->jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
+    HBX_HIP(hbx::run_jobs(pdx, jobs, n * G, reinterpret_cast<const uint32_t*>(m), tg,
                           intensity ? p->job_inten : nullptr, fo, st));
     double* cs = (env_ids || !chan_stats) ? chan_stats : chan_stats + (size_t)i0 * G * 3;
     double* ps = psnr ? (env_ids ? psnr : psnr + i0) : nullptr;
     EnvDev ed = dummy;
     if (env) ed = env_ids ? *env : env_offset(*env, i0, G * pd.P, G, pd.N);
-    HBX_HIP(hbx::launch_full_finalize(p->jobs, pd.job_stats, n, G, cs, ps, pixel_count(p),
-                                      p->optics.rel_scale, p->optics.peak, ed, env ? 1 : 0, st));
+    if (cs || ps || env)   // tt.simulate alone (fields only) has nothing to finalize
+      HBX_HIP(hbx::launch_full_finalize(jobs, pd.job_stats, n, G, cs, ps, pixel_count(p),
+                                        p->optics.rel_scale, p->optics.peak, ed, env ? 1 : 0, st));
     if (intensity) {
       float* cache = env_ids ? intensity : intensity + (size_t)i0 * G * pd.N * pd.N;
-      HBX_HIP(hbx::launch_scatter_intensity(p->jobs, n * G, p->job_inten, cache, G,
+      HBX_HIP(hbx::launch_scatter_intensity(jobs, n * G, p->job_inten, cache, G,
                                             (size_t)pd.N * pd.N, nullptr, st));
     }
   }
@@ -1177,6 +1187,34 @@ int hbx_plan_read_timing(hbx_plan_t p, double* ms_total, int64_t* launches, int6
     tm->calls[k] = 0;
     tm->jobs[k] = 0;
   }
+  return HBX_OK;
+}
+
+int hbx_pack_mask(const void* src, int32_t src_kind, int64_t n_values, int32_t mode, double threshold,
+                  uint64_t* bits, int32_t* error, void* stream) {
+  if (n_values < 0 || n_values % 64) return fail(HBX_ERR_INVALID, "hbx_pack_mask: n_values must be a multiple of 64");
+  if (n_values == 0) return HBX_OK;
+  if (!src || !bits) return fail(HBX_ERR_INVALID, "hbx_pack_mask: null buffer");
+  if (mode != HBX_PACK_BINARY && mode != HBX_PACK_THRESHOLD)
+    return fail(HBX_ERR_INVALID, "hbx_pack_mask: mode must be HBX_PACK_BINARY or HBX_PACK_THRESHOLD");
+  const uintptr_t align = src_kind == HBX_SRC_U8 ? 4 : src_kind == HBX_SRC_F32 ? 16 : src_kind == HBX_SRC_F64 ? 32 : 0;
+  if (!align) return fail(HBX_ERR_INVALID, "hbx_pack_mask: src_kind must be HBX_SRC_U8, _F32 or _F64");
+  if ((uintptr_t)src % align) return fail(HBX_ERR_INVALID, "hbx_pack_mask: src is not aligned to its vector load");
+  if ((uintptr_t)bits % 8) return fail(HBX_ERR_INVALID, "hbx_pack_mask: bits is not 8-byte aligned");
+  HBX_HIP(hbx::launch_pack_mask(src, src_kind, n_values / 64, mode, threshold, bits, error, (hipStream_t)stream));
+  return HBX_OK;
+}
+
+int hbx_rel_stats(const void* x, const void* y, int32_t src_kind, int64_t n, int32_t rel_scale, double peak,
+                  double* workspace, double* out, void* stream) {
+  static_assert(HBX_REL_WORKSPACE_DOUBLES >= 3 * 1024, "workspace holds 3 doubles per partial slot");
+  if (n <= 0) return fail(HBX_ERR_INVALID, "hbx_rel_stats: n must be > 0");
+  if (!x || !y || !workspace || !out) return fail(HBX_ERR_INVALID, "hbx_rel_stats: null buffer");
+  if (src_kind != HBX_SRC_F32 && src_kind != HBX_SRC_F64)
+    return fail(HBX_ERR_INVALID, "hbx_rel_stats: src_kind must be HBX_SRC_F32 or HBX_SRC_F64");
+  if (rel_scale != HBX_REL_NONE && rel_scale != HBX_REL_LSQ) return fail(HBX_ERR_INVALID, "hbx_rel_stats: rel_scale");
+  if (3 * hbx::rel_partial_slots() > HBX_REL_WORKSPACE_DOUBLES) return fail(HBX_ERR_INVALID, "workspace size");
+  HBX_HIP(hbx::launch_rel_stats(x, y, src_kind, n, (double)n, rel_scale, peak, workspace, out, (hipStream_t)stream));
   return HBX_OK;
 }
 

@@ -349,5 +349,11 @@ hipError_t launch_obs_sync(const int32_t* env_ids, int n_ids, const uint64_t* ma
                            hipStream_t st);
 hipError_t launch_obs_settle(const int32_t* env_ids, int n_ids, float* intensity, const float* recon,
                              int32_t* pending, int G, size_t hw, hipStream_t st);
+// (ABI v14) hbx_pack.hip: mask values -> bits, and relativeLoss statistics
+hipError_t launch_pack_mask(const void* src, int kind, int64_t n_words, int mode, double thr, uint64_t* bits,
+                            int32_t* err, hipStream_t st);
+int rel_partial_slots();
+hipError_t launch_rel_stats(const void* x, const void* y, int kind, int64_t n, double count, int rel_scale,
+                            double peak, double* part, double* out, hipStream_t st);
 
 }  // namespace hbx

@@ -11,11 +11,11 @@ The torchOptics-compatible operator shim lives in the sibling package
 from . import _lib
 from ._lib import (ACCEPT_DBS, ACCEPT_ENV, FIELD_AMPLITUDE, FIELD_PHASE, PRECISION_BF16_STORE,
                    PRECISION_F16_STORE, PRECISION_F32, REL_LSQ, REL_NONE, TF_ASM, TF_FRESNEL, HbxError)
-from .plan import (OpticsConfig, Plan, crop, crop_bits, crop_config, mono_config, pack_bits, rgb_config,
+from .plan import (OpticsConfig, Plan, crop, crop_bits, crop_config, mono_config, pack_bits, pack_mask, rgb_config,
                    unpack_bits)
 
 __all__ = [
-    "OpticsConfig", "Plan", "mono_config", "rgb_config", "pack_bits", "unpack_bits", "crop", "crop_bits",
+    "OpticsConfig", "Plan", "mono_config", "rgb_config", "pack_bits", "pack_mask", "unpack_bits", "crop", "crop_bits",
     "crop_config", "HbxError",
     "TF_ASM", "TF_FRESNEL", "FIELD_AMPLITUDE", "FIELD_PHASE", "REL_LSQ", "REL_NONE", "ACCEPT_ENV",
     "ACCEPT_DBS", "PRECISION_F32", "PRECISION_BF16_STORE", "PRECISION_F16_STORE", "load_library",

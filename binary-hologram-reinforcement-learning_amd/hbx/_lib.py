@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HBX_LIB", os.path.join(_HERE, "libhbx.so"))
 
 # constants mirrored from include/hbx.h
-ABI_VERSION = 13
+ABI_VERSION = 14
 OK = 0
 ERR_INVALID, ERR_HIP, ERR_UNSUPPORTED, ERR_NOMEM = -1, -2, -3, -4
 TF_ASM, TF_FRESNEL = 0, 1
@@ -26,6 +26,9 @@ WALK_MAX_K = 256           # hbx_dbs_walk_psf speculation depth bound
 WALK_FUSED_K = (1, 2, 3, 4)   # one launch per batch (two accepts resolved for K = 2..4)
 PRECISION_F32, PRECISION_BF16_STORE, PRECISION_F16_STORE = 0, 1, 2   # hbx_plan_set_precision
 OBS_STATE, OBS_RECON, OBS_RESOLVE, OBS_SETTLE = 1, 2, 4, 8   # hbx_env_obs_sync
+SRC_U8, SRC_F32, SRC_F64 = 0, 1, 2             # hbx_pack_mask / hbx_rel_stats value kinds (ABI v14)
+PACK_BINARY, PACK_THRESHOLD = 0, 1
+REL_WORKSPACE_DOUBLES = 3072
 
 EXPORTED_SYMBOLS = (
     "hbx_abi_version", "hbx_last_error", "hbx_plan_create", "hbx_plan_destroy",
@@ -35,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "hbx_eval_flips_psf", "hbx_commit_flip_psf", "hbx_dbs_walk_psf",
     "hbx_plan_set_precision", "hbx_plan_precision", "hbx_env_obs_sync",
     "hbx_planes_fill", "hbx_eval_flips_planes", "hbx_commit_flip_planes", "hbx_dbs_walk_planes",
-    "hbx_dbs_walk_planes_fill", "hbx_host_alloc", "hbx_host_free",
+    "hbx_dbs_walk_planes_fill", "hbx_host_alloc", "hbx_host_free", "hbx_pack_mask", "hbx_rel_stats",
 )
 NUM_PASSES = 5
 PASS_NAMES = ("k_rowfwd", "k_col", "k_rowinv", "k_psf_eval", "k_psf_commit")
@@ -137,6 +140,8 @@ def _declare(lib):
                                              I64, I64, VP]
     lib.hbx_host_alloc.argtypes = [C.c_size_t, C.POINTER(VP), C.POINTER(VP)]
     lib.hbx_host_free.argtypes = [VP]
+    lib.hbx_pack_mask.argtypes = [VP, I32, I64, I32, C.c_double, VP, VP, VP]
+    lib.hbx_rel_stats.argtypes = [VP, VP, I32, I64, I32, C.c_double, VP, VP, VP]
     lib.hbx_plan_set_timing.argtypes = [VP, I32]
     lib.hbx_plan_set_timing_sampled.argtypes = [VP, I32, I32]
     lib.hbx_plan_read_timing.argtypes = [VP, C.POINTER(C.c_double), C.POINTER(C.c_int64),

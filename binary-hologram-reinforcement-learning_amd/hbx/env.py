@@ -24,7 +24,7 @@ import torch
 
 from . import _lib
 from . import spaces
-from .plan import OpticsConfig, Plan, mono_config, pack_bits, rgb_config, unpack_bits
+from .plan import OpticsConfig, Plan, mono_config, pack_mask, rgb_config, unpack_bits
 
 RW = 800.0   # env.py:29
 
@@ -95,7 +95,150 @@ class LazyObs(dict):
         return [(k, self[k]) for k in self.keys()]
 
     def device(self, k):
+        """Key `k` as a device tensor.  Like the numpy values it shows THIS step's data for as long
+        as the caller keeps it: a key still aliasing an env buffer the next step rewrites is
+        snapshotted (one device copy) first, so the tensor handed out never changes under the
+        caller."""
+        if k not in self._owned and dict.__getitem__(self, k) is None:
+            self._t[k] = self._t[k].clone()
+            self._owned.add(k)
         return self._t[k]
+
+
+class HostObsMirror:
+    """obs_format="numpy" observations kept on the HOST and updated by the rules the reference
+    applies to its own host arrays (env.py:164-181), so a step moves only recon_image device ->
+    host (r06):
+
+    * state_record[b, 0, c, r, col] += 1 for every env's action (an attempt, env.py:165; int8
+      wraps like numpy's), state[b, 0, c, r, col] ^= accepted[b] (env.py:164, 191-196);
+    * pre_model / target_image change only at a reset (env.py:107,111): the reset envs' rows are
+      copied from the device once, with state from the device mask mirror and state_record = 0;
+    * recon_image is the one per-step device -> host copy, queued behind the step into pinned
+      memory (env.py:179 `result_after.cpu().numpy()`).
+
+    Two host sets alternate (ping-pong): each step / reset writes the set the previous call did
+    NOT return, so the observation a caller still holds -- SB3 adds `self._last_obs` to its
+    rollout buffer AFTER the next env.step() -- keeps its values until the call after next.  A
+    set catches up on the changes it missed (the other set's last step delta and resets) in
+    order before it is written; a checkpoint load invalidates both (full re-copy)."""
+
+    def __init__(self, vec: "HologramVecEnv"):
+        self.vec = vec
+        c = vec.cfg
+        B = vec.num_envs
+        self.keys = tuple(vec.obs_keys)
+        self.shapes = {"state_record": ((B, 1, c.channels, c.height, c.width), np.int8),
+                       "state": ((B, 1, c.channels, c.height, c.width), np.int8),
+                       "pre_model": ((B, 1, c.channels, c.height, c.width), np.float32),
+                       "target_image": ((B, 1, c.groups, c.height, c.width), np.float32),
+                       "recon_image": ((B, 1, c.groups, c.height, c.width), np.float32)}
+        self.sets = [None, None]
+        self._recon_t = [None, None]      # pinned torch tensors behind the recon arrays
+        self.cur = 1                      # begin() switches to set 0 first
+        self.pending = [[], []]
+        self.valid = [False, False]
+        self.d2h_bytes = 0                # device -> host bytes of the last call
+
+    def _alloc(self, s):
+        if self.sets[s] is not None:
+            return
+        d = {}
+        for k in self.keys:
+            shape, dt = self.shapes[k]
+            if k == "recon_image":
+                t = torch.empty(shape, dtype=torch.float32, pin_memory=True)
+                self._recon_t[s] = t
+                d[k] = t.numpy()
+            else:
+                d[k] = np.empty(shape, dt)
+        self.sets[s] = d
+
+    def _dev(self, k):
+        st = self.vec.state
+        return {"state_record": st.record, "state": st.state_bytes, "pre_model": st.pre_model,
+                "target_image": st.target, "recon_image": st.recon}[k]
+
+    def _copy_rows_from_device(self, s, ids):
+        d = self.sets[s]
+        idx = None if ids is None else torch.as_tensor(ids, dtype=torch.int64, device=self.vec.device)
+        for k in self.keys:
+            src = self._dev(k)
+            rows = src if idx is None else src.index_select(0, idx)
+            h = rows.cpu().numpy().reshape((rows.shape[0],) + d[k].shape[1:])
+            self.d2h_bytes += h.nbytes
+            if idx is None:
+                d[k][...] = h
+            else:
+                d[k][ids] = h
+
+    def _apply(self, s, op):
+        d = self.sets[s]
+        if op[0] == "d":
+            _, b, c, r, col, acc = op
+            if "state_record" in d:
+                d["state_record"][b, 0, c, r, col] += np.int8(1)
+            if "state" in d:
+                d["state"][b, 0, c, r, col] ^= acc
+        else:                             # ("r", ids): rows of a reset, from the set that took it
+            _, ids = op
+            o = self.sets[1 - s]
+            for k in d:
+                d[k][ids] = o[k][ids]
+
+    def begin(self):
+        """Switch to the other set and bring it up to date; returns its index."""
+        s = 1 - self.cur
+        self._alloc(s)
+        self.d2h_bytes = 0
+        if not self.valid[s]:
+            self._copy_rows_from_device(s, None)
+            self.valid[s] = True
+            self.pending[s] = []
+        else:
+            for op in self.pending[s]:
+                self._apply(s, op)
+            self.pending[s] = []
+        self.cur = s
+        return s
+
+    def queue_recon(self):
+        """The step's recon_image device -> host copy into the current set (async, pinned)."""
+        if "recon_image" in self.keys:
+            t = self._recon_t[self.cur]
+            t.copy_(self.vec.state.recon.reshape(t.shape), non_blocking=True)
+            self.d2h_bytes += t.numel() * 4
+
+    def step_delta(self, actions: np.ndarray, accepted: np.ndarray):
+        c = self.vec.cfg
+        hw = c.height * c.width
+        ch, pix = np.divmod(actions.astype(np.int64), hw)
+        r, col = np.divmod(pix, c.width)
+        op = ("d", np.arange(self.vec.num_envs), ch, r, col, (accepted != 0).astype(np.int8))
+        self._apply(self.cur, op)
+        self.pending[1 - self.cur].append(op)
+
+    def reset_rows(self, ids):
+        ids = list(ids)
+        if not ids:
+            return
+        if not self.valid[self.cur]:      # a full copy picks the reset rows up too
+            return
+        self._copy_rows_from_device(self.cur, ids)
+        self.pending[1 - self.cur].append(("r", np.asarray(ids, np.int64)))
+
+    def sync_recon(self):
+        """A reset-only call: the whole recon_image from the device (blocking)."""
+        if "recon_image" in self.keys and self.valid[self.cur]:
+            self.queue_recon()
+            torch.cuda.current_stream(self.vec.device).synchronize()
+
+    def invalidate(self):
+        self.valid = [False, False]
+        self.pending = [[], []]
+
+    def obs(self) -> dict:
+        return dict(self.sets[self.cur])
 
 
 class EnvState:
@@ -328,6 +471,9 @@ class HologramVecEnv(_VecEnvBase):
         self._settle_args = None
         self._obs_views = None
         self._lazy_ref = None      # the last LazyObs handed out (obs_format="lazy")
+        self._in_step = False
+        # obs_format="numpy": host mirrors updated by the reference's rules, recon the only D2H
+        self._mirror = HostObsMirror(self) if obs_format == "numpy" else None
         self.episode_count = 0
         if HAVE_SB3:  # pragma: no cover - SB3 absent here
             _VecEnvBase.__init__(self, self.num_envs, self.observation_space, self.action_space)
@@ -348,7 +494,7 @@ class HologramVecEnv(_VecEnvBase):
         pre = torch.as_tensor(pre).to(self.device, torch.float32).reshape(c.channels, c.height, c.width)
         st = self.state
         st.target[i].copy_(tgt[0])
-        st.mask[i].copy_(pack_bits(pre >= 0.5))                       # env.py:120
+        pack_mask(pre, threshold=0.5, out=st.mask[i])                  # env.py:120, one HIP launch
         if st.pre_model is not None:
             st.pre_model[i].copy_(pre)
         self.episode_count += 1
@@ -373,6 +519,8 @@ class HologramVecEnv(_VecEnvBase):
         self.plan.env_reset(self.state.bufs, self.num_envs, idt)      # env.py:121-133
         if self.importance_samples:
             self._importance_reset(ids)
+        if self._mirror is not None:
+            self._mirror.reset_rows(ids)          # the reset rows' host observations, once
 
     def _importance_reset(self, ids):
         """env_group.py:90-143,198 for the listed envs (see hbx/importance.py)."""
@@ -395,12 +543,16 @@ class HologramVecEnv(_VecEnvBase):
         """VecEnv.reset: every env; returns the batched observation (obs_format).
         Seeds given through seed() are recorded and consumed here (the reference
         ignores reset's seed, env.py:90 -- SURVEY F9)."""
+        if self._mirror is not None:
+            self._mirror.begin()
         self.reset_envs(range(self.num_envs))
         self._seeds = [None for _ in range(self.num_envs)]
         self.reset_infos = [{} for _ in range(self.num_envs)]
         return self._format(self.observe(stepped=False))
 
     def _format(self, obs: dict):
+        if self._mirror is not None:
+            return self._mirror.obs()
         if self.obs_format == "numpy":
             return _to_numpy(obs)
         if self.obs_format == "lazy":
@@ -436,6 +588,8 @@ class HologramVecEnv(_VecEnvBase):
                                   (a[:, 0] * c.height + a[:, 1]) * c.width + a[:, 2])
         actions = actions.reshape(self.num_envs).contiguous()
         self._before_launch(STEP_OBS_KEYS)
+        if self._mirror is not None and not self._in_step:
+            self._mirror.invalidate()             # a bare device step: the host mirrors re-copy once
         if out is None:
             out = (self._reward, self._psnr, self._acc, self._term, self._trunc)
         else:
@@ -539,27 +693,32 @@ class HologramVecEnv(_VecEnvBase):
         key = self._graph_key()
         if self._graph_h is not None and self._graph_h_key != key:
             self._graph_h = None
+        # the last LazyObs snapshots its unread keys BEFORE anything is captured or replayed: a
+        # snapshot taken inside the capture would be recorded into the graph and re-run by every
+        # replay
+        self._before_launch(STEP_OBS_KEYS)
         if self._graph_h is None:
             if not self._graph_h_warm:
                 # lazy plan buffers are allocated on the first step: run one eagerly
-                self._launch_fast(self._arow.device)
+                self._launch_fast(self._arow.device, snapshot=False)
                 self._graph_h_warm = True
                 return
             g = torch.cuda.CUDAGraph()
             st = torch.cuda.Stream(device=self.device)
             st.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.graph(g, stream=st):
-                self._launch_fast(self._arow.device)
+                self._launch_fast(self._arow.device, snapshot=False)
             torch.cuda.current_stream(self.device).wait_stream(st)
             self._graph_h, self._graph_h_key = g, key
-        self._before_launch(STEP_OBS_KEYS)
         self._graph_h.replay()
 
-    def _launch_fast(self, actions_ptr: int):
+    def _launch_fast(self, actions_ptr: int, snapshot: bool = True):
         """hbx_env_step on the current stream with the results written into the host-mapped
         row; `actions_ptr` is any address the kernels can read B int64 actions from (a device
-        tensor, or host-mapped memory: BinaryHologramEnv)."""
-        self._before_launch(STEP_OBS_KEYS)
+        tensor, or host-mapped memory: BinaryHologramEnv).  snapshot=False: the caller already
+        ran the LazyObs snapshot (graph capture must not record it)."""
+        if snapshot:
+            self._before_launch(STEP_OBS_KEYS)
         # the prebuilt argument list holds pointers to env.params / env.state.bufs: rebuilt when
         # either object is replaced (ADVICE r04: a new EnvParams must not be silently ignored)
         ids = (id(self.params), id(self.state.bufs))
@@ -592,20 +751,43 @@ class HologramVecEnv(_VecEnvBase):
         if rc != _lib.OK:
             _lib.check(rc, "hbx_env_obs_sync(SETTLE)")
 
+    def _actions_host(self, actions) -> np.ndarray:
+        """The step's flat actions as numpy int64 (the host mirrors' decode)."""
+        a = actions.detach().cpu().numpy() if isinstance(actions, torch.Tensor) else np.asarray(actions)
+        a = a.astype(np.int64)
+        if self.action_format == "multidiscrete":
+            c = self.cfg
+            a = a.reshape(self.num_envs, 3)
+            return (a[:, 0] * c.height + a[:, 1]) * c.width + a[:, 2]
+        return a.reshape(self.num_envs)
+
     def step(self, actions):
         """SB3 VecEnv.step: (obs, rewards[B], dones[B], infos) with auto-reset
         (done envs report their last observation as info["terminal_observation"])."""
-        if self._host_actions(actions):
+        m = self._mirror
+        if m is not None:
+            m.begin()
+        hostpath = self._host_actions(actions)
+        a_host = None
+        if m is not None:
+            a_host = self._act_np.copy() if hostpath else self._actions_host(actions)
+        if hostpath:
             if self.use_graph and self.device.type == "cuda":
                 self._graph_fast()
             else:
                 self._launch_fast(self._arow.device)
         elif not self._fast_step(actions):
-            self.step_device(actions)
+            self._in_step = True
+            try:
+                self.step_device(actions)
+            finally:
+                self._in_step = False
             # the other paths write the device row: one device -> host copy (rewards, done flags,
             # the error word), queued behind the step
             self._host_t.copy_(self._out_raw, non_blocking=True)
         n = self.num_envs
+        if m is not None:
+            m.queue_recon()                       # recon_image D2H behind the step, before the wait
         # the observation views and infos are built while the step is in flight
         if self._readback is not None:
             self._readback.record()
@@ -618,15 +800,22 @@ class HologramVecEnv(_VecEnvBase):
             # 256x8 step, profiles/r04/step_host_r04g.txt) and would burn a core
             self._readback.synchronize()
         if self._h_err[0]:
+            if m is not None:
+                m.invalidate()
             self.state.check_error()                      # clears the word and raises
+        if m is not None:
+            m.step_delta(a_host, self._host_np[16 * n:17 * n])
         r = self._h_rew.copy() if self.obs_format == "torch" else self._h_rew.astype(np.float32)
         dones = np.logical_or(self._h_term, self._h_trunc)   # the kernels write 0 / 1
         if self.auto_reset and dones.any():
             t, tr = self._h_term != 0, self._h_trunc != 0
             done_ids = np.nonzero(dones)[0].tolist()
-            term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}
-            if self.obs_format != "torch":
-                term_obs = _to_numpy(term_obs)
+            if m is not None:
+                term_obs = {k: v[done_ids] for k, v in m.obs().items()}   # fancy index: copies
+            else:
+                term_obs = {k: v[done_ids].clone() for k, v in obs.items()} if obs else {}
+                if self.obs_format != "torch":
+                    term_obs = _to_numpy(term_obs)
             for j, i in enumerate(done_ids):
                 infos[i]["terminal_observation"] = {k: v[j] for k, v in term_obs.items()}
                 infos[i]["TimeLimit.truncated"] = bool(tr[i] and not t[i])
@@ -687,10 +876,16 @@ class HologramVecEnv(_VecEnvBase):
         object called once per requested env."""
         idx = self._indices(indices)
         if method_name == "reset":
+            if self._mirror is not None:
+                self._mirror.begin()
             self.reset_envs(idx)
-            obs = self.observe(stepped=False)
-            if self.obs_format != "torch":
-                obs = _to_numpy(obs)
+            if self._mirror is not None:
+                self._mirror.sync_recon()
+                obs = self._mirror.obs()
+            else:
+                obs = self.observe(stepped=False)
+                if self.obs_format != "torch":
+                    obs = _to_numpy(obs)
             return [{k: v[i] for k, v in obs.items()} for i in idx]
         if method_name in ("render", "get_images"):
             return [None for _ in idx]
@@ -785,6 +980,8 @@ class HologramVecEnv(_VecEnvBase):
                (_lib.OBS_RECON if st.recon is not None and not have_recon else 0)
         if what:
             self.plan.env_obs_sync(st.bufs, self.num_envs, what)
+        if self._mirror is not None:
+            self._mirror.invalidate()
 
     # -- gym-ish accessors ------------------------------------------------------------
     @property

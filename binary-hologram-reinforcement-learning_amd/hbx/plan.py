@@ -90,13 +90,57 @@ def _need(t: torch.Tensor, name: str, dtype: torch.dtype, shape, device: torch.d
         raise ValueError(f"{name} must be contiguous")
 
 
+_PACK_KIND = {torch.bool: _lib.SRC_U8, torch.int8: _lib.SRC_U8, torch.uint8: _lib.SRC_U8,
+              torch.float32: _lib.SRC_F32, torch.float64: _lib.SRC_F64}
+_PACK_ALIGN = {_lib.SRC_U8: 4, _lib.SRC_F32: 16, _lib.SRC_F64: 32}
+
+
+def pack_mask(values: torch.Tensor, threshold: Optional[float] = None, out: Optional[torch.Tensor] = None,
+              error_ptr: Optional[int] = None, stream=None) -> torch.Tensor:
+    """Device tensor [..., H, W] -> int64 words [..., H, W/64] with ONE HIP launch
+    (hbx_pack_mask, ABI v14; bit j of word w = column 64 w + j).
+
+    threshold None: bit = (v != 0), and a value other than 0 / 1 stores 1 at `error_ptr`
+    (an address the kernel may write: device or host-mapped memory) -- tt.simulate's binary
+    check without a host sync.  threshold t: bit = (v >= t) -- env.py:120's `pre_model >= 0.5`.
+    bool / int8 / uint8 / float32 / float64 are read as they are; other dtypes are converted
+    to float32 on the device first.  `out`: a contiguous int64 tensor of the result's shape."""
+    if not values.is_cuda:
+        raise ValueError("pack_mask runs on the GPU (hbx_pack_mask); pack_bits packs host tensors")
+    w = values.shape[-1]
+    if w % 64:
+        raise ValueError("width must be a multiple of 64")
+    kind = _PACK_KIND.get(values.dtype)
+    if kind is None:
+        values, kind = values.to(torch.float32), _lib.SRC_F32
+    if not values.is_contiguous() or values.data_ptr() % _PACK_ALIGN[kind]:
+        values = values.contiguous() if not values.is_contiguous() else values.clone()
+    shape = (*values.shape[:-1], w // 64)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.int64, device=values.device)
+    elif tuple(out.shape) != shape or out.dtype != torch.int64 or not out.is_contiguous() \
+            or out.device != values.device:
+        raise ValueError(f"pack_mask out: a contiguous int64 {shape} tensor on {values.device}")
+    lib = _lib.load()
+    mode = _lib.PACK_BINARY if threshold is None else _lib.PACK_THRESHOLD
+    s = stream.cuda_stream if stream is not None else torch._C._cuda_getCurrentRawStream(values.device.index)
+    rc = lib.hbx_pack_mask(values.data_ptr(), kind, values.numel(), mode,
+                           0.0 if threshold is None else float(threshold), out.data_ptr(), error_ptr, s)
+    if rc != _lib.OK:
+        _lib.check(rc, "hbx_pack_mask")
+    return out
+
+
 def pack_bits(mask: torch.Tensor) -> torch.Tensor:
     """{0,1} tensor [..., H, W] -> int64 words [..., H, W/64] (bit j of word w = col 64w+j).
 
-    Runs on the tensor's device (torch ops; layout of include/hbx.h)."""
+    GPU tensors: one hbx_pack_mask launch (bit = v != 0).  Host tensors (test fixtures,
+    checkpoint tooling) are packed with torch ops on the CPU."""
     w = mask.shape[-1]
     if w % 64:
         raise ValueError("width must be a multiple of 64")
+    if mask.is_cuda:
+        return pack_mask(mask)
     m = (mask != 0).to(torch.int64).reshape(*mask.shape[:-1], w // 64, 64)
     shifts = torch.arange(64, device=mask.device, dtype=torch.int64)
     return (m << shifts).sum(dim=-1, dtype=torch.int64)   # bit 63 wraps into the sign: same bits

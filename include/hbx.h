@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HBX_ABI_VERSION 13
+#define HBX_ABI_VERSION 14
 
 #define HBX_OK 0
 #define HBX_ERR_INVALID (-1)     /* bad argument / shape                          */
@@ -512,6 +512,40 @@ int hbx_plan_set_timing_sampled(hbx_plan_t plan, int32_t capacity, int32_t every
  * time, launches[HBX_NUM_PASSES], jobs[HBX_NUM_PASSES] = summed jobs per
  * launch; then clears the record. */
 int hbx_plan_read_timing(hbx_plan_t plan, double* ms_total, int64_t* launches, int64_t* jobs);
+
+/* (ABI v14) Mask -> bits on the device, one streaming pass (hbx_pack.hip).  Replaces the
+ * per-call host / torch work in front of every propagation: env reset's `state =
+ * (pre_model >= 0.5)` (env.py:120, env_1024_24.py:120-124) and the float / int8 mask that
+ * tt.simulate receives (env.py:123,170-171 `tt.Tensor(torch.tensor(state, float32))`;
+ * DBS_1024_24.py:326-327).
+ *   src      `n_values` contiguous values of kind src_kind (HBX_SRC_U8: bool / int8 / uint8
+ *            bytes; HBX_SRC_F32; HBX_SRC_F64), aligned to 4 (u8) / 16 (f32) / 32 (f64) bytes;
+ *            n_values % 64 == 0 (rows of W values with W % 64 == 0 are contiguous words)
+ *   bits     n_values / 64 words in the mask layout above (bit j of word w = value 64 w + j)
+ *   mode     HBX_PACK_BINARY: bit = (v != 0); a value that is not 0 or 1 (NaN included)
+ *            stores 1 into *error (nullable; any address the kernel may write, e.g. host
+ *            memory from hbx_host_alloc, so the check needs no device -> host copy).
+ *            HBX_PACK_THRESHOLD: bit = (v >= threshold) (NaN -> 0, as torch's `>=`).
+ * Runs on the current device, asynchronously on `stream`; no plan needed. */
+#define HBX_SRC_U8 0
+#define HBX_SRC_F32 1
+#define HBX_SRC_F64 2
+#define HBX_PACK_BINARY 0
+#define HBX_PACK_THRESHOLD 1
+int hbx_pack_mask(const void* src, int32_t src_kind, int64_t n_values, int32_t mode, double threshold,
+                  uint64_t* bits, int32_t* error, void* stream);
+
+/* (ABI v14) tt.relativeLoss(x, y, tm.get_PSNR / F.mse_loss) (env.py:131-132,174;
+ * DBS_1024_24.py:332,342,352) in one fixed-order f64 reduction: x, y `n` contiguous values
+ * of kind HBX_SRC_F32 or HBX_SRC_F64 (both the same kind);
+ *   out[5] = {sum x y, sum x^2, sum y^2, PSNR, MSE}  with the plans' rel_scale rule
+ *   (HBX_REL_LSQ: s = sum xy / sum x^2, MSE = mean((s x - y)^2); HBX_REL_NONE: s = 1) and
+ *   PSNR = 10 log10(peak^2 / MSE) (+inf at MSE <= 0).
+ * `workspace` holds HBX_REL_WORKSPACE_DOUBLES doubles (device); `out` any address the kernel
+ * may write (host-mapped memory reads back without a copy). */
+#define HBX_REL_WORKSPACE_DOUBLES 3072
+int hbx_rel_stats(const void* x, const void* y, int32_t src_kind, int64_t n, int32_t rel_scale, double peak,
+                  double* workspace, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,32 @@ int main(void) {
   CHECK(hbx_plan_workspace_bytes(NULL) == 0);
   CHECK(hbx_plan_destroy(NULL) == HBX_OK);
 
+  /* (ABI v14) pack / relativeLoss: argument validation before any launch */
+  {
+    static double buf[8];   /* 32-byte aligned enough for every kind; never dereferenced */
+    void* src = (void*)(((unsigned long)buf + 31) & ~31ul);
+    uint64_t* bits = (uint64_t*)src;
+    CHECK(hbx_pack_mask(src, HBX_SRC_F32, 0, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) == HBX_OK); /* empty */
+    CHECK(hbx_pack_mask(src, HBX_SRC_F32, 100, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) == HBX_ERR_INVALID);
+    CHECK(strstr(hbx_last_error(), "multiple of 64") != NULL);
+    CHECK(hbx_pack_mask(NULL, HBX_SRC_F32, 64, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_pack_mask(src, HBX_SRC_F32, 64, HBX_PACK_BINARY, 0.0, NULL, NULL, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_pack_mask(src, 7, 64, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_pack_mask(src, HBX_SRC_F32, 64, 5, 0.0, bits, NULL, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_pack_mask((char*)src + 4, HBX_SRC_F32, 64, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) ==
+          HBX_ERR_INVALID);
+    CHECK(strstr(hbx_last_error(), "aligned") != NULL);
+    CHECK(hbx_pack_mask((char*)src + 16, HBX_SRC_F64, 64, HBX_PACK_THRESHOLD, 0.5, bits, NULL, NULL) ==
+          HBX_ERR_INVALID);
+    CHECK(hbx_pack_mask((char*)src + 2, HBX_SRC_U8, 64, HBX_PACK_BINARY, 0.0, bits, NULL, NULL) ==
+          HBX_ERR_INVALID);
+    CHECK(hbx_rel_stats(src, src, HBX_SRC_F32, 0, HBX_REL_LSQ, 1.0, buf, buf, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_rel_stats(NULL, src, HBX_SRC_F32, 64, HBX_REL_LSQ, 1.0, buf, buf, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_rel_stats(src, src, HBX_SRC_F32, 64, HBX_REL_LSQ, 1.0, NULL, buf, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_rel_stats(src, src, HBX_SRC_U8, 64, HBX_REL_LSQ, 1.0, buf, buf, NULL) == HBX_ERR_INVALID);
+    CHECK(hbx_rel_stats(src, src, HBX_SRC_F32, 64, 3, 1.0, buf, buf, NULL) == HBX_ERR_INVALID);
+  }
+
   /* plan validation happens before any device call */
   hbx_plan_t p = NULL;
   hbx_optics_t o = rgb(1024);

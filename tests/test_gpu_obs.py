@@ -428,3 +428,94 @@ def test_dropin_graph_replay_equals_eager():
     assert envs[1]._vec._graph_h is not None and ended
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("N,G,steps", [(256, 1, 300), (64, 3, 200)])
+def test_numpy_obs_host_mirrors_equal_torch_obs(N, G, steps):
+    """obs_format="numpy" (VERDICT r05 #4): host mirrors updated by env.py:164-181's rules, only
+    recon_image copied device -> host per step.  Against a twin env with obs_format="torch": every
+    key equal at every step across rollbacks and auto-resets; an observation the caller holds
+    keeps its values through the next step (SB3 adds _last_obs after the following step); the
+    per-step D2H is recon alone; terminal observations match; a bare step_device re-syncs the
+    mirrors."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.mono_config(N) if G == 1 else hbx.OpticsConfig(N, N, 3, 2, hbx.plan.WL_RGB)
+    B = 6
+    g = torch.Generator(device="cuda").manual_seed(41 + N)
+    pres = [torch.rand((cfg.channels, N, N), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, N, N), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=37, obs_keys=OBS_KEYS)
+    ref = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    npy = HologramVecEnv(cfg, B, lambda i: tgts[i], obs_format="numpy", **kw)
+    o_ref, o_np = ref.reset(), npy.reset()
+    for k in OBS_KEYS:
+        assert isinstance(o_np[k], np.ndarray) and np.array_equal(o_np[k], o_ref[k].cpu().numpy()), k
+    acts = torch.randint(0, cfg.channels * N * N, (steps, B), generator=g, device="cuda")
+    acts_h = acts.cpu().numpy()
+    held, held_want = None, None
+    n_done = n_rej = 0
+    recon_bytes = B * cfg.groups * N * N * 4
+    resync = False
+    for s in range(steps):
+        o1, r1, d1, i1 = ref.step(acts[s])
+        o2, r2, d2, i2 = npy.step(acts_h[s])
+        assert np.array_equal(r1.astype(np.float32), r2) and np.array_equal(d1, d2), s
+        for k in OBS_KEYS:
+            assert np.array_equal(o2[k], o1[k].cpu().numpy()), (s, k)
+        if held is not None:                      # the obs returned one step ago is unchanged
+            for k in OBS_KEYS:
+                assert np.array_equal(held[k], held_want[k]), (s, k)
+        held, held_want = o2, {k: v.copy() for k, v in o2.items()}
+        n_rej += int((~ref.last_step()["accepted"]).sum())
+        if d1.any():
+            n_done += int(d1.sum())
+            for i in np.nonzero(d1)[0]:
+                for k in OBS_KEYS:
+                    assert np.array_equal(i2[i]["terminal_observation"][k],
+                                          i1[i]["terminal_observation"][k].cpu().numpy()), (s, i, k)
+        elif not resync:
+            assert npy._mirror.d2h_bytes == recon_bytes, s
+        resync = s == steps // 2
+        if resync:                                # a bare device step: the next step re-copies
+            ref.step_device(acts[s])
+            npy.step_device(acts[s])
+    assert n_done > 0 and n_rej > 0
+    ref.close()
+    npy.close()
+
+
+def test_graph_lazy_obs_snapshot_not_recorded():
+    """graph=True + obs_format='lazy' + numpy actions.  An observation left unread
+    across two more steps still shows its own step's data (the snapshot runs before the capture,
+    not inside the graph), and device() hands out a stable copy, not the live buffer."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.mono_config(256)
+    B = 4
+    g = torch.Generator(device="cuda").manual_seed(29)
+    pres = [torch.rand((cfg.channels, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, 256, 256), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=False, obs_keys=OBS_KEYS)
+    eager = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    lazy = HologramVecEnv(cfg, B, lambda i: tgts[i], obs_format="lazy", graph=True, **kw)
+    eager.reset()
+    lazy.reset()
+    acts = torch.randint(0, cfg.channels * 256 * 256, (12, B), generator=g, device="cuda").cpu().numpy()
+    kept = []
+    for s in range(12):
+        o1, _, _, _ = eager.step(acts[s])
+        o2, _, _, _ = lazy.step(acts[s])
+        want = {k: o1[k].cpu().numpy().copy() for k in OBS_KEYS}
+        dev = o2.device("state") if s % 3 == 0 else None
+        kept.append((o2, want, dev))
+        if len(kept) > 2:
+            old, old_want, old_dev = kept[-3]
+            for k in OBS_KEYS:
+                assert np.array_equal(old[k], old_want[k]), (s, k)
+            if old_dev is not None:
+                assert np.array_equal(old_dev.cpu().numpy(), old_want["state"]), s
+                assert old_dev.data_ptr() != lazy.state.state_bytes.data_ptr()
+    assert lazy._graph_h is not None
+    eager.close()
+    lazy.close()

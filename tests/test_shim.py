@@ -56,7 +56,7 @@ def test_simulate_matches_oracle():
     u3 = tt.simulate(tt.Tensor(m[:, :3], meta=x.meta), 2e-3)
     assert np.max(np.abs(u3[0].cpu().numpy() - want[:3])) <= 2e-5 * np.max(np.abs(want))
     with pytest.raises(ValueError):
-        tt.simulate(tt.Tensor(np.full((1, 2, 64, 64), 0.5, np.float32), meta=x.meta), 2e-3)
+        tt.simulate(tt.Tensor(np.full((1, 2, 64, 64), 0.5, np.float32), meta=x.meta), 2e-3, strict=True)
 
 
 @pytest.mark.gpu
