@@ -1222,6 +1222,21 @@ def main():
                         "(64 px per side), FFT mode, same env semantics; 896 = 28 x 32 mixed-radix passes "
                         "(csrc/hbx_passes896.hip)"}
         torch.cuda.empty_cache()
+        if not args.no_planes:
+            # (r06) the plane-cached FFT mode at 896: the FFT mode's bits (tests/test_gpu_planes.py)
+            psteps = 4 * args.steps
+            vec, dt, timing, acc_rate = measure("planes", psteps, args.warmup, mcfg=ccfg, margin=64)
+            vec.close()
+            if rank == 0:
+                ps = pass_table(timing, plane_cached_bytes(cN, P))
+                pms = dt / psteps * 1e3
+                out["crop_896"]["plane_cached_mode"] = {
+                    "value": round(B * world * psteps / dt, 2), "unit": "env-steps/s", "steps": psteps,
+                    "ms_per_step": round(pms, 4), "accept_rate": round(acc_rate, 4),
+                    "vs_fft_mode": round((B * world * psteps / dt) / out["crop_896"]["value"], 3),
+                    "passes": rounded(ps),
+                    "step_alg_GBs": round(sum(plane_cached_bytes(cN, P).values()) * B / (pms * 1e-3) / 1e9, 1)}
+            torch.cuda.empty_cache()
 
     if not args.no_ppo:
         # SURVEY 3.2 / BASELINE configs[3]'s per-GPU shard: train-PPO.py's env (env.py, 256x256x8

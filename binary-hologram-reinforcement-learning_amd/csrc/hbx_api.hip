@@ -215,6 +215,9 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   if (hipMalloc(&p->jobs, (size_t)max_jobs * sizeof(JobDesc)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "jobs");
   if (hipMalloc(&p->full_jobs, (size_t)max_jobs * sizeof(JobDesc)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "full jobs");
+  // the plane-cache walk's arrival counter (zero between launches; its user resets it): allocated
+  // and zeroed here, not on a walk's first call (no blocking memset inside a hot / captured call)
+  if (hipMalloc(&p->planes_ticket, 64) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "walk ticket");
   if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "accept_flag");
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
@@ -228,6 +231,7 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       hipMemcpy(pd.htab, ht.data(), ht.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(pd.zero_row, 0, (size_t)N * sizeof(float)) != hipSuccess ||
+      hipMemset(p->planes_ticket, 0, 64) != hipSuccess ||
       hbx::launch_jobs_full(nullptr, max_jobs / G, G, p->full_jobs, nullptr) != hipSuccess ||
       hipStreamSynchronize(nullptr) != hipSuccess)
     return cleanup(HBX_ERR_HIP, "table upload");
@@ -412,7 +416,8 @@ int propagate_full(hbx_plan_t p, const uint64_t* mask, const float* target, cons
   const PlanDev& pd = p->pd;
   const int CHs = pd.G * pd.P + 2 * spares;   // plane-cache slots per env
   if (plane_pool) {                           // identity slots, then every plane's |U|^2 into its slot
-    if (pd.R != 32 && pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+    if (pd.R != 32 && pd.R != 16 && pd.R != 0)
+      return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024, 896 or 256 only");
     HBX_HIP(hbx::launch_plane_slot_init(env_ids, n_ids, plane_slot, CHs, st));
   }
   const int G = pd.G;
@@ -690,7 +695,8 @@ int hbx_env_step(hbx_plan_t p, const hbx_env_buffers_t* e, const hbx_env_params_
   if ((e->plane_inten != nullptr) != (e->plane_slot != nullptr))
     return fail(HBX_ERR_INVALID, "plane cache: give both plane_inten and plane_slot");
   const bool planes = e->plane_inten != nullptr;
-  if (planes && pd.R != 32 && pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (planes && pd.R != 32 && pd.R != 16 && pd.R != 0)
+    return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024, 896 or 256 only");
   if (planes) pdx.plane_mode = hbx::kPlanesStep;
   EnvParams ep;
   ep.max_steps = prm->max_steps; ep.t_psnr = prm->t_psnr; ep.t_steps = prm->t_steps;
@@ -889,7 +895,8 @@ int hbx_eval_flips_planes(hbx_plan_t p, const uint64_t* base_mask, const float* 
   if (K <= 0) return K == 0 ? HBX_OK : fail(HBX_ERR_INVALID, "K");
   if (!base_mask || !target || !base_chan_stats || !plane_inten || !plane_slot || !flips || !psnr_out)
     return fail(HBX_ERR_INVALID, "null buffer");
-  if (p->pd.R != 32 && p->pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (p->pd.R != 32 && p->pd.R != 16 && p->pd.R != 0)
+    return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024, 896 or 256 only");
   if (K > n_spare_pairs) return fail(HBX_ERR_INVALID, "K > n_spare_pairs: every candidate needs its own spare pair");
   HBX_HIP(hipSetDevice(p->device));
   hipStream_t st = (hipStream_t)stream;
@@ -950,7 +957,8 @@ int hbx_dbs_walk_planes_fill(hbx_plan_t p, uint64_t* base_mask, const float* tar
     return fail(HBX_ERR_INVALID, "null buffer");
   if (accept_cap < 0 || (accept_cap > 0 && (!accept_pos || !accept_psnr)))
     return fail(HBX_ERR_INVALID, "accept log");
-  if (p->pd.R != 32 && p->pd.R != 16) return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024 or 256 only");
+  if (p->pd.R != 32 && p->pd.R != 16 && p->pd.R != 0)
+    return fail(HBX_ERR_UNSUPPORTED, "plane cache: N = 1024, 896 or 256 only");
   if (K < 1 || K > 256 || K > p->max_jobs || K > n_spare_pairs)
     return fail(HBX_ERR_INVALID, "K must be in [1, min(256, max_jobs, n_spare_pairs)]");
   if (batches < 0 || n_order < 0) return fail(HBX_ERR_INVALID, "batches / n_order");
@@ -967,11 +975,7 @@ int hbx_dbs_walk_planes_fill(hbx_plan_t p, uint64_t* base_mask, const float* tar
   pdx.plane_spares = n_spare_pairs;
   pdx.spare_base = 0;
   pdx.skip_reduce = 1;                     // the decision reduces the row-block partials itself
-  const int RB = pd.N / (256 / pd.R);
-  if (!p->planes_ticket) {   // the fused decision's arrival counter (first call only; reset by its user)
-    if (hipMalloc(&p->planes_ticket, 64) != hipSuccess) return fail(HBX_ERR_NOMEM, "walk ticket");
-    if (hipMemset(p->planes_ticket, 0, 64) != hipSuccess) return fail(HBX_ERR_HIP, "walk ticket");
-  }
+  const int RB = pd.R ? pd.N / (256 / pd.R) : pd.N / 8;
   hbx::WalkPlanesArgs wa;
   wa.w = walk; wa.order = order; wa.jobs = p->jobs; wa.partial = pd.partial; wa.mask = base_mask;
   wa.base_stats = base_chan_stats; wa.plane_slot = plane_slot; wa.accept_pos = accept_pos;
@@ -980,12 +984,16 @@ int hbx_dbs_walk_planes_fill(hbx_plan_t p, uint64_t* base_mask, const float* tar
   wa.count = pixel_count(p); wa.rel_scale = p->optics.rel_scale; wa.peak = p->optics.peak;
   wa.fill_count = fill_count; wa.fill_target = fill_target; wa.fill_tol = fill_tol;
   // (r05) each batch's decision runs in the last-arriving k_rowinv_d workgroup of that batch
-  // (k_rowinv_d<R, true>): three launches per batch instead of four
-  pdx.walk_planes = &wa;
+  // (k_rowinv_d<R, true>): three launches per batch instead of four.  (r06) N = 896: the decision
+  // in a launch of its own behind each batch (k_walk_planes, decide = 1)
+  const bool fused = pd.R != 0;
+  pdx.walk_planes = fused ? &wa : nullptr;
   HBX_HIP(hbx::launch_walk_planes(wa, 0, st));   // this call's first batch of jobs, from the walk state
-  for (int b = 0; b < batches; ++b)
+  for (int b = 0; b < batches; ++b) {
     HBX_HIP(hbx::run_jobs(pdx, p->jobs, K, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,
                           nullptr, st));
+    if (!fused) HBX_HIP(hbx::launch_walk_planes(wa, 1, st));
+  }
   return HBX_OK;
 }
 

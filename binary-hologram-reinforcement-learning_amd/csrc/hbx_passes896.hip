@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
                                                       const uint32_t* __restrict__ mask,
                                                       float2* __restrict__ ws_a,
                                                       const float2* __restrict__ tw_glob, int P, int CH,
-                                                      float va, float vb) {
+                                                      float va, float vb, int pair_step) {
   constexpr int SCRF = kGPB * kR * (kR + 1);      // floats: 8 FFT tiles (33.8 KB)
   static_assert(kHalf * kGPB * 2 <= SCRF, "one plane's tile must fit in the FFT tiles");
   constexpr int RBW = kRB / kRit896;
@@ -111,10 +111,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
   int bid = blockIdx.x;
   const int rbw = bid % RBW;
   bid /= RBW;
-  const int q = bid % (P / 2);
-  const int j = bid / (P / 2);
+  const int npair = pair_step ? 1 : P / 2;   // (r06) plane-cached step: only the flipped plane's pair
+  const int j = bid / npair;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;  // uniform per block
+  const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
   const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * kN * kWPR;
   const int wt = t < kWPR ? t : kWPR - 1;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
                                                    const float2* __restrict__ ws_a,
                                                    float2* __restrict__ ws_b,
                                                    const float2* __restrict__ htab,
-                                                   const float2* __restrict__ tw_glob, int P) {
+                                                   const float2* __restrict__ tw_glob, int P, int pair_step) {
   __shared__ float2 tw[kN];
   __shared__ float2 scratch[kSCR];
   for (int i = threadIdx.x; i < kN; i += 256) tw[i] = tw_glob[i];
@@ -240,10 +241,11 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
   int bid = blockIdx.x;
   const int lb = bid % kColLB;
   bid /= kColLB;
-  const int p = bid % P;
-  const int j = bid / P;
+  const int np = pair_step ? 2 : P;     // (r06) plane-cached step: the flipped plane's pair only
+  const int j = bid / np;
   const JobDesc jb = jobs[j];
   if (jb.env < 0) return;
+  const int p = pair_step ? (jb.flip_plane & ~1) + bid % 2 : bid % np;
   const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * kPlaneA, (unsigned)(kPlaneA * 8));
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * kPlaneB, (unsigned)(kPlaneB * 8));
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (kHalf + 1) * kN,
@@ -353,7 +355,10 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
                                                       double* __restrict__ partial,
                                                       float* __restrict__ inten_out,
                                                       float2* __restrict__ field_out, size_t tmask,
-                                                      int inten_by_env) {
+                                                      int inten_by_env, int plane_mode,
+                                                      float* __restrict__ plane_pool,
+                                                      const int32_t* __restrict__ plane_slot, int plane_spares,
+                                                      int spare_base) {
   constexpr int TL = 8;                           // slots per tile (1-KB tiles, as N = 1024)
   __shared__ float2 tw[kN];
   __shared__ float2 scratch[kSCR];
@@ -398,20 +403,61 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
 #pragma unroll
   for (int k = 0; k < kL; ++k) acc[k] = 0.0f;
   const PaddedScratch<kR> sc{scratch + grp * kR * (kR + 1)};
-  float2 v[32];
-  load_plane(v, 0);
-  __syncthreads();  // tw visible
-#pragma unroll 1
-  for (int p = 0; p < P; ++p) {
+  // (r06) plane cache, as k_rowinv_d (hbx_passes.hip): slots of this env's planes, pool rows of this
+  // lane group's row y; every plane's |U_p|^2 goes to its slot on a fill, the flipped pair's two to
+  // the job's spare pair on a step, and a step adds the cached planes in the FFT mode's plane order
+  const int CH = G * P;
+  const int CHS = CH + 2 * (plane_spares > 1 ? plane_spares : 1);
+  const int spare = CH + 2 * (plane_spares > 1 ? spare_base + j : 0);
+  const int32_t* slots = plane_slot ? plane_slot + (size_t)jb.env * CHS : nullptr;
+  auto pool_row = [&](int slot) { return plane_pool + (((size_t)jb.env * CHS + slot) * kN + y) * kN; };
+  auto finish_plane = [&](float2 (&v)[32], int p) {
     fft896_sn<true, kInvScalar>(v, t, sc, tw);      // slot layout in, natural out: x = t + 32 j
+    float f[kL];
 #pragma unroll
-    for (int k = 0; k < kL; ++k) acc[k] += fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+    for (int k = 0; k < kL; ++k) {
+      f[k] = fmaf(v[k].x, v[k].x, v[k].y * v[k].y);
+      acc[k] += f[k];
+    }
     if (field_out) {  // exact field of this plane (incremental mode init / refresh)
       float2* frow = field_out + (((size_t)jb.env * G * P + jb.group * P + p) * kN + y) * kN;
 #pragma unroll
       for (int k = 0; k < kL; ++k) frow[t + kR * k] = v[k];
     }
-    load_plane(v, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
+    if (plane_mode != kPlanesOff) {
+      float* orow = pool_row(slots[plane_mode == kPlanesFill ? jb.group * P + p : spare + (p & 1)]);
+#pragma unroll
+      for (int k = 0; k < kL; ++k) __builtin_nontemporal_store(f[k], orow + t + kR * k);
+    }
+  };
+  auto add_cached = [&](int q) {
+    const float* crow = pool_row(slots[jb.group * P + q]);
+    float c[kL];
+#pragma unroll
+    for (int k = 0; k < kL; ++k) c[k] = __builtin_nontemporal_load(crow + t + kR * k);
+#pragma unroll
+    for (int k = 0; k < kL; ++k) acc[k] += c[k];
+  };
+  float2 v[32];
+  if (plane_mode == kPlanesStep) {   // only the flipped plane's pair is in B
+    const int pa = jb.flip_plane & ~1;
+    load_plane(v, pa);
+    __syncthreads();  // tw visible
+#pragma unroll 1
+    for (int q = 0; q < pa; ++q) add_cached(q);
+    finish_plane(v, pa);
+    load_plane(v, pa + 1);
+    finish_plane(v, pa + 1);
+#pragma unroll 1
+    for (int q = pa + 2; q < P; ++q) add_cached(q);
+  } else {
+    load_plane(v, 0);
+    __syncthreads();  // tw visible
+#pragma unroll 1
+    for (int p = 0; p < P; ++p) {
+      finish_plane(v, p);
+      load_plane(v, p + 1 < P ? p + 1 : p);   // unconditional: the last round re-reads plane P - 1
+    }
   }
 
   const float invp = 1.0f / (float)P;
@@ -456,19 +502,23 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
   const int P = pd.P;
   const int CH = pd.G * pd.P;
   PassTimer* tm = pd.timer;
+  // (r06) plane-cached mode at 896: a fill writes every plane's |U|^2, a step propagates the
+  // flipped plane's pair only (the walk's decision runs in a launch of its own at 896)
+  const int pair = pd.plane_mode == kPlanesStep ? 1 : 0;
+  if (pd.plane_mode != kPlanesOff && (!pd.plane_pool || !pd.plane_slot)) return hipErrorInvalidValue;
   if (tm) tm->begin(0, st);
-  hipLaunchKernelGGL(k_rowfwd896, dim3((unsigned)n_jobs * (P / 2) * (kRB / kRit896)), dim3(256), 0, st, jobs, mask,
-                     pd.ws_a,
-                     pd.tw, P, CH, pd.va, pd.vb);
+  hipLaunchKernelGGL(k_rowfwd896, dim3((unsigned)n_jobs * (pair ? 1 : P / 2) * (kRB / kRit896)), dim3(256), 0, st,
+                     jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair);
   if (tm) tm->end(0, n_jobs, st);
   if (tm) tm->begin(1, st);
-  hipLaunchKernelGGL(k_col896, dim3((unsigned)n_jobs * P * kColLB), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b,
-                     pd.htab, pd.tw, P);
+  hipLaunchKernelGGL(k_col896, dim3((unsigned)n_jobs * (pair ? 2 : P) * kColLB), dim3(256), 0, st, jobs, pd.ws_a,
+                     pd.ws_b, pd.htab, pd.tw, P, pair);
   if (tm) tm->end(1, n_jobs, st);
   if (tm) tm->begin(2, st);
   hipLaunchKernelGGL(k_rowinv896, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
                      target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
-                     target ? ~(size_t)0 : (size_t)0, pd.inten_by_env);
+                     target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot,
+                     pd.plane_spares, pd.spare_base);
   if (tm) tm->end(2, n_jobs, st);
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial, n_jobs, kRB,
                      pd.job_stats);

@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .env import PLANE_SIZES
 from .plan import Plan
 
 OUTPUT_BINS = np.round(np.linspace(0, 1.0, 11), decimals=10)   # DBS_1024_24.py:209
@@ -661,9 +662,9 @@ def greedy(plan: Plan, mask: torch.Tensor, target: torch.Tensor, order, stop_dif
     order_t = torch.as_tensor(np.asarray(order, np.int64)).to(dev)
     total = int(order_t.shape[0]) if max_candidates is None else min(int(order_t.shape[0]), max_candidates)
     if planes is None:
-        planes = mode == "fft" and plan.cfg.height in (256, 1024)
-    if planes and (mode != "fft" or plan.cfg.height not in (256, 1024)):
-        raise ValueError("planes=True is the FFT mode's plane cache at N = 1024 / 256")
+        planes = mode == "fft" and plan.cfg.height in PLANE_SIZES
+    if planes and (mode != "fft" or plan.cfg.height not in PLANE_SIZES):
+        raise ValueError("planes=True is the FFT mode's plane cache at N = 1024 / 896 / 256")
     if device_walk is None:
         device_walk = planes
     if device_walk:

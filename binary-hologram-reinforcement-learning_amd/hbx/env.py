@@ -30,6 +30,7 @@ RW = 800.0   # env.py:29
 
 OBS_KEYS = ("state_record", "state", "pre_model", "recon_image", "target_image")
 STEP_OBS_KEYS = ("state_record", "state", "recon_image")   # the buffers a step rewrites
+PLANE_SIZES = (256, 896, 1024)   # N with the plane-cached FFT mode (896: r06)
 
 # SB3's VecEnv base class when stable-baselines3 is importable (train-PPO.py:296-322 hands the
 # env to PPO; optimize_hyperparameter.py:317-318 wraps it in VecNormalize), so isinstance checks
@@ -361,8 +362,8 @@ class HologramVecEnv(_VecEnvBase):
             raise ValueError("give exactly one of pre_model_fn(target) or pre_model_source(env_index)")
         if mode not in ("fft", "psf", "planes"):
             raise ValueError(f"mode must be 'fft', 'psf' or 'planes', got {mode!r}")
-        if mode == "planes" and cfg.height not in (256, 1024):
-            raise ValueError("mode='planes' is built for N = 256 and 1024")
+        if mode == "planes" and cfg.height not in PLANE_SIZES:
+            raise ValueError("mode='planes' is built for N = 256, 896 and 1024")
         if mode == "psf" and "recon_image" in obs_keys:
             raise ValueError("mode='psf' does not produce the pre-rollback recon_image observation; "
                              "drop it from obs_keys or use mode='fft'")
@@ -1098,7 +1099,7 @@ class BinaryHologramEnv(spaces.EnvBase):
         # mask and recon bit for bit the FFT mode's (tests/test_gpu_planes.py), one plane pair
         # propagated per step -- 14.5k vs 13.9k steps/s at 256x8, 3.18k vs 2.97k at 1024x24 (B = 1,
         # profiles/r05/dropin_modes_r05aj.txt).  mode="fft" re-propagates the whole group.
-        vec_kwargs.setdefault("mode", "planes" if self.cfg.height in (256, 1024) else "fft")
+        vec_kwargs.setdefault("mode", "planes" if self.cfg.height in PLANE_SIZES else "fft")
         if vec_kwargs.get("mode", "fft") == "psf":
             raise ValueError("BinaryHologramEnv returns the stepped recon_image (env.py:179): mode 'fft' or 'planes'")
         if "obs_keys" in vec_kwargs:

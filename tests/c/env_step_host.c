@@ -169,6 +169,35 @@ int main(int argc, char** argv) {
   EXPECT(*(const int32_t*)(h + eoff) != 0);
   EXPECT(h[16 * (size_t)B + 0] == 0);   /* the offending env's step is a no-op */
 
+  /* HBX_OBS_SETTLE validates its buffers before the one-group no-op, so argument errors
+   * are the same at every G (this plan has G = 1 and the env no recon / intensity / recon_pending) */
+  EXPECT(hbx_env_obs_sync(plan, &e, B, NULL, 0, HBX_OBS_SETTLE, st) == HBX_ERR_INVALID);
+  EXPECT(strstr(hbx_last_error(), "HBX_OBS_SETTLE") != NULL);
+
+  /* (ABI v14) the pack kernel from plain C: 0/1 bytes -> words, and the binary check's word */
+  {
+    const size_t nv = 4 * 64 + 64;           /* 5 words: a ragged last group of the kernel */
+    uint8_t hv[320];
+    for (size_t i = 0; i < nv; ++i) hv[i] = (uint8_t)((i * 7 + i / 3) % 2);
+    uint8_t* dv = (uint8_t*)dalloc(nv);
+    uint64_t* dw = (uint64_t*)dalloc(5 * 8);
+    EXPECT(dv && dw);
+    CHECK_HIP(hipMemcpy(dv, hv, nv, hipMemcpyHostToDevice));
+    int32_t* herr = (int32_t*)(h + eoff);
+    *herr = 0;
+    CHECK_HBX(hbx_pack_mask(dv, HBX_SRC_U8, (int64_t)nv, HBX_PACK_BINARY, 0.0, dw, (int32_t*)(d + eoff), st));
+    CHECK_HIP(hipStreamSynchronize(st));
+    uint64_t hw5[5];
+    CHECK_HIP(hipMemcpy(hw5, dw, sizeof hw5, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nv; ++i) EXPECT(((hw5[i / 64] >> (i % 64)) & 1u) == hv[i]);
+    EXPECT(*herr == 0);
+    hv[nv - 1] = 2;
+    CHECK_HIP(hipMemcpy(dv, hv, nv, hipMemcpyHostToDevice));
+    CHECK_HBX(hbx_pack_mask(dv, HBX_SRC_U8, (int64_t)nv, HBX_PACK_BINARY, 0.0, dw, (int32_t*)(d + eoff), st));
+    CHECK_HIP(hipStreamSynchronize(st));
+    EXPECT(*herr == 1);
+  }
+
   printf("env_step_host: %d envs x %d steps of 256x256x8 in %.3f s (%.0f env-steps/s incl. one host "
          "round trip per step), %ld accepted / %ld rolled back, max |prev_psnr - fresh| = %.3g dB, OK\n",
          B, n_steps, sec, B * n_steps / sec, n_acc, n_rej, worst);

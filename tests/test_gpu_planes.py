@@ -34,10 +34,12 @@ def _same_state(a, b, what):
         assert torch.equal(getattr(sa, k), getattr(sb, k)), (what, k)
 
 
-@pytest.mark.parametrize("N,B,steps,max_steps", [(1024, 4, 120, 10000), (256, 16, 300, 40)])
+@pytest.mark.parametrize("N,B,steps,max_steps", [(1024, 4, 120, 10000), (256, 16, 300, 40), (896, 4, 120, 50)])
 def test_planes_mode_bit_exact_vs_fft_mode(N, B, steps, max_steps):
+    """N = 896 (r06): the 64-pixel centre crop of env_1024_24_128.py:144-149 on the mixed-radix
+    28 x 32 passes, whose plane-cached step is built the same way (hbx_passes896.hip)."""
     import hbx
-    cfg = hbx.rgb_config(1024) if N == 1024 else hbx.mono_config(256)
+    cfg = hbx.mono_config(256) if N == 256 else hbx.rgb_config(N)
     fft, planes, g = _pair(cfg, B, 5 + N, max_steps=max_steps)
     o1, o2 = fft.reset(), planes.reset()
     assert torch.equal(o1["recon_image"], o2["recon_image"])
@@ -136,3 +138,23 @@ def test_planes_mode_rejects_unbuilt_sizes_and_half_buffers():
     env.state.bufs.plane_slot = None                                     # pool without slot table
     with pytest.raises(RuntimeError):
         env.step_device(torch.zeros(2, dtype=torch.int64, device="cuda"))
+
+
+def test_planes_896_greedy_walk_equals_host_batches():
+    """(r06) the FFT-mode greedy DBS on the plane cache at N = 896 (DBS_1024_24-128.py's crop): the
+    device walk (its decision in a launch of its own behind each batch at 896) and the full
+    re-propagation per candidate (planes=False) give the same accept sequence and PSNR bits."""
+    import hbx
+    from hbx import dbs
+    cfg = hbx.rgb_config(896)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    pre = torch.rand((cfg.channels, 896, 896), generator=g, device="cuda")
+    tgt = torch.rand((cfg.groups, 896, 896), generator=g, device="cuda")
+    mask = hbx.pack_mask(pre, threshold=0.5)
+    order = np.random.default_rng(3).permutation(cfg.channels * 896 * 896)[:1500]
+    plan = hbx.Plan(cfg, max_jobs=8)
+    walk = dbs.greedy(plan, mask.clone(), tgt, order=order, mode="fft", planes=True)
+    ref = dbs.greedy(plan, mask.clone(), tgt, order=order, mode="fft", planes=False, k_max=8)
+    assert walk.accepted_positions == ref.accepted_positions and len(walk.accepted_positions) > 0
+    assert walk.final_psnr == ref.final_psnr
+    plan.close()
