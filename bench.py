@@ -793,6 +793,7 @@ def reset_cost(cfg, n_env: int = 8, reps: int = 5):
     shipped (hbx_pack_mask, one HIP launch, ABI v14) and as it was through r05 (torch ops:
     `(pre >= 0.5)` -> int64 -> shift -> sum, several kernels materialising 8 B per pixel) --
     the same reset otherwise, alternated, median of `reps`."""
+    import statistics
     import torch
     import hbx.env as E
     from hbx.env import HologramVecEnv

@@ -193,7 +193,11 @@ class HostObsMirror:
         self._alloc(s)
         self.d2h_bytes = 0
         if not self.valid[s]:
-            self._copy_rows_from_device(s, None)
+            if self.valid[1 - s]:        # the other set is current: a host copy, no device traffic
+                for k, v in self.sets[1 - s].items():
+                    np.copyto(self.sets[s][k], v)
+            else:
+                self._copy_rows_from_device(s, None)
             self.valid[s] = True
             self.pending[s] = []
         else:

@@ -19,8 +19,10 @@ def main():
         for rep in range(2):
             out[f"torch_reference_step_{rep}"] = bench.torch_reference_step(256, 300, 20)["value"]
             out[f"shim_dbs_loop_{rep}"] = bench.shim_dbs_loop(256, 300, 20)["value"]
+        print(json.dumps(out), flush=True)
     if "reset" in what:
         out["reset_1024x24"] = bench.reset_cost(rgb_config(1024))
+        print(json.dumps(out), flush=True)
     if "numpy" in what:
         mono = mono_config(256)
         g = torch.Generator(device="cuda").manual_seed(3)
@@ -28,7 +30,7 @@ def main():
         tgts = [torch.rand((1, 256, 256), generator=g, device="cuda") for _ in range(128)]
         out["vecenv_step_obs_numpy"] = bench.vecenv_step_obs_numpy(mono, 128, 30, 5, lambda i: tgts[i],
                                                                    lambda i: pres[i], 13)
-    print(json.dumps(out))
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
