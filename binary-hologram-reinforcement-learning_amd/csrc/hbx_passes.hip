@@ -96,6 +96,12 @@ struct TileB {
 template <int R>
 constexpr bool kTiledB = R == 32 || R == 16;
 
+#ifdef HBX_ROWINV_LEAN
+constexpr bool HBX_ROWINV_LEAN_ON = true;
+#else
+constexpr bool HBX_ROWINV_LEAN_ON = false;
+#endif
+
 // ---------------------------------------------------------------------------
 // Pass 1
 // ---------------------------------------------------------------------------
@@ -463,6 +469,14 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   using PB = LayoutB<R>;   // B planes: N lines
   const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * plane_a_elems(R), plane_a_elems(R) * 8);
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
+#ifdef HBX_COL2_RSRC
+  // the B plane's address as a wave-uniform (SGPR) value: per-round descriptors are SALU adds
+  const uint64_t bsg = [&] {
+    const uint64_t a = reinterpret_cast<uint64_t>(ws_b + ((size_t)j * P + p) * plane_b_elems(R));
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)a);
+  }();
+#endif
   // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
   const PaddedScratch<R> sc{scratch + grp * RS};
@@ -542,7 +556,11 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       const int kxb = kx - grp;            // the block's GPB lines: slot tile kxb / GPB
       col2_stage_write<R, SK>(v, 1.0f, scratch, grp, t);
       lds_barrier();
+#ifdef HBX_COL2_RSRC
+      col2_stage_store_p<R>(scratch, bsg, kxb / GPB);
+#else
       col2_stage_store<R>(scratch, rb, kxb / GPB);
+#endif
       if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
         const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
@@ -553,7 +571,11 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       fft_group_s2<R, true, true>(w, t, sc);
       col2_stage_write<R, SK>(w, sy, scratch, grp, t);
       lds_barrier();
+#ifdef HBX_COL2_RSRC
+      col2_stage_store_p<R>(scratch, bsg, (N / 2 + kxb) / GPB);
+#else
       col2_stage_store<R>(scratch, rb, (N / 2 + kxb) / GPB);
+#endif
     } else {
       {
         const int vo = PB::voff(t, kx);
@@ -670,7 +692,7 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
 // plane's FFT is done (two blocks per CU cover them; a second register set for a plane in
 // flight took one block per CU and measured 1.80 ms against 1.47).  The r02
 // kernel staged every plane through an LDS tile between three block barriers (1.80 ms).
-template <int R, bool WALK = false>
+template <int R, bool WALK = false, bool LEAN = false>
 __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__ jobs,
                                                      const float2* __restrict__ ws_b,
                                                      const float* __restrict__ target,
@@ -706,6 +728,12 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
     }
     if constexpr (WALK) walk_planes_arrive(wk, reinterpret_cast<char*>(scratch));
     return;
+  }
+  if constexpr (LEAN) {   // the plain FFT-mode launch: no plane cache, field, reconcile or walk code
+    plane_mode = kPlanesOff;
+    field_out = nullptr;
+    rc_pending = nullptr;
+    rc_cache = nullptr;
   }
   const int y = rb * GPB + grp;
   constexpr int PLB = N * N;                 // float2 per B plane
@@ -1106,6 +1134,12 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
                            target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,
                            pd.plane_slot, pd.plane_spares, pd.spare_base, pd.rc_pending, pd.rc_cache,
                            *pd.walk_planes);
+      } else if (HBX_ROWINV_LEAN_ON && pd.plane_mode == kPlanesOff && !field_out && !pd.rc_pending) {
+        hipLaunchKernelGGL((k_rowinv_d<R, false, true>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
+                           target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                           target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,
+                           pd.plane_slot, pd.plane_spares, pd.spare_base, pd.rc_pending, pd.rc_cache,
+                           WalkPlanesArgs{});
       } else {
         hipLaunchKernelGGL((k_rowinv_d<R>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
                            target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,

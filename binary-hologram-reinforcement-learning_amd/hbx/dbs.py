@@ -413,7 +413,7 @@ def walk_k_planes(q: float, groups: int = 3, k_min: int = 1, k_max: int = 64, ta
     q = min(max(q, 1e-6), 1.0)
     # one pass of planes_visited's recursion gives the visited count of every k (the host runs
     # this once per 64-batch chunk: the per-k recomputation, O(k_max^2), took ~12 ms at k_max =
-    # 256 and starved the GPU, 260 vs 78 us per batch, profiles/r04/walk_kmax_r04i.txt)
+    # 256 and starved the GPU, 260 vs 78 us per batch, profiles/archive/r04/walk_kmax_r04i.txt)
     best, bk = math.inf, k_min
     dist = [1.0] + [0.0] * groups
     vis = 0.0
@@ -540,7 +540,7 @@ def _walk_stream(device, i: int):
     (measured at 1024x24, 32,768 candidates per image: 2 walks 95k, 3 walks 178k, 4 walks
     190k candidates/s aggregate).  HBX_WALK_STREAMS=n: walk i on stream i % n of a per-device
     pool created in one go (2 walks 154k, 3 walks 180k, 4 walks 148k) -- better for two
-    images, worse for the default four (profiles/r02_walk/walk_streams.txt)."""
+    images, worse for the default four (profiles/archive/r02_walk/walk_streams.txt)."""
     dev = torch.device(device)
     n = os.environ.get("HBX_WALK_STREAMS", "")
     if not n.isdigit() or int(n) < 1:

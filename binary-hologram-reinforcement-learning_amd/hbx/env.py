@@ -802,7 +802,7 @@ class HologramVecEnv(_VecEnvBase):
         infos = [{} for _ in range(self.num_envs)]
         if self._readback is not None:
             # a blocking wait: spinning on ev.query() measured no faster (0.3303 vs 0.3276 ms per
-            # 256x8 step, profiles/r04/step_host_r04g.txt) and would burn a core
+            # 256x8 step, profiles/archive/r04/step_host_r04g.txt) and would burn a core
             self._readback.synchronize()
         if self._h_err[0]:
             if m is not None:

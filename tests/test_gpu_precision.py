@@ -3,11 +3,11 @@ sweep) at the headline size.
 
 r03 found the bf16 study variant of k_col2 at N = 1024 non-deterministic while the rounding sat
 between the staged LDS read and the non-temporal tile store (launch-to-launch differences of ~0.4 %
-in the channel sums, profiles/r03/bf16_determinism_r03f.txt); the f32 product path was
+in the channel sums, profiles/archive/r03/bf16_determinism_r03f.txt); the f32 product path was
 deterministic in every check.  The rounding now happens where each lane writes its line into the
 staging region.  These tests pin what the precision sweep relies on: a bf16 group propagation is a
 function of its inputs alone, and a flip's PSNR change under bf16 stays within the measured error
-of the f32 one (3.0e-7 dB rms, 1.3e-6 dB max over 2,048 flips; profiles/r03/bench_r03g.json).
+of the f32 one (3.0e-7 dB rms, 1.3e-6 dB max over 2,048 flips; profiles/archive/r03/bench_r03g.json).
 """
 import numpy as np
 import pytest

@@ -2,7 +2,7 @@
 
 r03: the bf16 / fp16 study variants of k_col2<32> were non-deterministic at N = 1024 because the
 compiler placed a VALU write of a 128-bit store's data VGPR right behind the store
-(`buffer_store_dwordx4 v[0:3] ... nt` -> `v_bfe_u32 v0, ...`; profiles/r03/bf16_determinism_r03f.txt,
+(`buffer_store_dwordx4 v[0:3] ... nt` -> `v_bfe_u32 v0, ...`; profiles/archive/r03/bf16_determinism_r03f.txt,
 DESIGN.md 4g).  tools/hazard_scan.py finds such pairs; the product code must have none."""
 import os
 import shutil

@@ -7,9 +7,9 @@ stores whose soffset is a constant, but EXEMPTS a MUBUF store with a register so
 schedules VALU writes of the data VGPRs straight behind the store (checked with a test kernel:
 soffset 0 -> `s_nop 1`, soffset s0 -> nothing).  Both r03 wrong-result events had exactly that
 code: the bf16 study variant of k_col2<32> (non-deterministic, `buffer_store_dwordx4 v[0:3], ...,
-s1 offen nt` -> `v_bfe_u32 v0, ...`; profiles/r03/bf16_determinism_r03f.txt) and the ITER = 1
+s1 offen nt` -> `v_bfe_u32 v0, ...`; profiles/archive/r03/bf16_determinism_r03f.txt) and the ITER = 1
 k_col2<16> build (wrong B rows, `buffer_store_dwordx4 v[32:35], ..., s11 offen nt` ->
-`v_add_f32_e32 v32, ...`; profiles/r03/kcol2_iter1_anomaly.txt), and neither hazard shows in
+`v_add_f32_e32 v32, ...`; profiles/archive/r03/kcol2_iter1_anomaly.txt), and neither hazard shows in
 the builds that were exact.
 
 Two rules, both must hold in every product kernel:

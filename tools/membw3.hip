@@ -139,7 +139,7 @@ template <int TL>
 __device__ __forceinline__ size_t tile_at(int line, int y) {
   return ((size_t)(y / 16) * (N / TL) + line / TL) * (16 * TL) + (y % 16) * TL + line % TL;
 }
-template <int TL>
+template <int TL, int PA = 8>
 __global__ __launch_bounds__(TL * 32, 1) void k_col2_tiled(const float2* __restrict__ A, float2* __restrict__ B) {
   constexpr int NT = TL * 32, ITER = 4, LB = (N / 2) / (TL * ITER), KSTEP = LB * TL;
   constexpr size_t PLA = (size_t)(N / 2) * N, PLB = (size_t)N * N;
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(TL * 32, 1) void k_col2_tiled(const float2* __restr
     const int kx = kx0 + grp;
     float2 v[R];
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) v[jj] = a[pan_at<8, N / 2>(kx, t + R * jj)];
+    for (int jj = 0; jj < R; ++jj) v[jj] = a[pan_at<PA, N / 2>(kx, t + R * jj)];
     for (int set = 0; set < 2; ++set) {
       lds_barrier();
       // tile element (band, r, l): band * 16 TL + r * TL + (l ^ (r & (TL - 1)))  (xor swizzle on the line)
@@ -366,6 +366,10 @@ int main() {
     time("rowinv_pan16", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_rows<16>), jobs * (N / 8), 256, 0, 0, B, o); });
     time("col2_T8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8>), gcol, 256, 0, 0, A, B); });
     time("col2_T16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<16>), gcol / 2, 512, 0, 0, A, B); });
+    // (r06) A in taller panels: k_col2's line reads become 128-B / 256-B pieces
+    time("col2_T8_A16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8, 16>), gcol, 256, 0, 0, A, B); });
+    time("col2_T8_A32", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8, 32>), gcol, 256, 0, 0, A, B); });
+    time("col2_T16_A16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<16, 16>), gcol / 2, 512, 0, 0, A, B); });
     time("col2_T8_direct8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<false>), gcol, 256, 0, 0, A, B); });
     time("col2_T8_swap16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<true>), gcol, 256, 0, 0, A, B); });
     time("rowinv_direct_pan16", (double)b_bytes, [&] { hipLaunchKernelGGL(k_rowinv_direct_pan16, jobs * (N / 8), 256, 0, 0, B, o); });

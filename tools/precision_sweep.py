@@ -17,7 +17,7 @@ decision flips sign.
 
 Each variant runs in its own child process (HBX_LIB selects the library);
 the parent touches no GPU.  Output: one JSON document on stdout.
-usage: python tools/precision_sweep.py [--out profiles/r01_precision.json]
+usage: python tools/precision_sweep.py [--out profiles/archive/r01_precision.json]
 """
 import argparse
 import json
