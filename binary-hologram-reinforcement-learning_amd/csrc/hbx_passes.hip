@@ -96,11 +96,7 @@ struct TileB {
 template <int R>
 constexpr bool kTiledB = R == 32 || R == 16;
 
-#ifdef HBX_ROWINV_LEAN
-constexpr bool HBX_ROWINV_LEAN_ON = true;
-#else
-constexpr bool HBX_ROWINV_LEAN_ON = false;
-#endif
+
 
 // ---------------------------------------------------------------------------
 // Pass 1
@@ -469,14 +465,6 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   using PB = LayoutB<R>;   // B planes: N lines
   const __amdgpu_buffer_rsrc_t ra = plane_rsrc(ws_a + ((size_t)j * P + p) * plane_a_elems(R), plane_a_elems(R) * 8);
   const __amdgpu_buffer_rsrc_t rb = plane_rsrc(ws_b + ((size_t)j * P + p) * plane_b_elems(R), plane_b_elems(R) * 8);
-#ifdef HBX_COL2_RSRC
-  // the B plane's address as a wave-uniform (SGPR) value: per-round descriptors are SALU adds
-  const uint64_t bsg = [&] {
-    const uint64_t a = reinterpret_cast<uint64_t>(ws_b + ((size_t)j * P + p) * plane_b_elems(R));
-    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-           __builtin_amdgcn_readfirstlane((uint32_t)a);
-  }();
-#endif
   // H rows of this group, natural [kx][ky]: element (kx, t + R k2) at (kx N + t) * 8 + k2 * R * 8
   const __amdgpu_buffer_rsrc_t rh = plane_rsrc(htab + (size_t)jb.group * (N / 2 + 1) * N, (N / 2 + 1) * N * 8);
   const PaddedScratch<R> sc{scratch + grp * RS};
@@ -556,11 +544,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       const int kxb = kx - grp;            // the block's GPB lines: slot tile kxb / GPB
       col2_stage_write<R, SK>(v, 1.0f, scratch, grp, t);
       lds_barrier();
-#ifdef HBX_COL2_RSRC
-      col2_stage_store_p<R>(scratch, bsg, kxb / GPB);
-#else
       col2_stage_store<R>(scratch, rb, kxb / GPB);
-#endif
       if (it + 1 < ITER) {  // next line in flight under the second inverse FFT
         const int vo = PA::voff(t, kx + KSTEP);
 #pragma unroll
@@ -571,11 +555,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
       fft_group_s2<R, true, true>(w, t, sc);
       col2_stage_write<R, SK>(w, sy, scratch, grp, t);
       lds_barrier();
-#ifdef HBX_COL2_RSRC
-      col2_stage_store_p<R>(scratch, bsg, (N / 2 + kxb) / GPB);
-#else
       col2_stage_store<R>(scratch, rb, (N / 2 + kxb) / GPB);
-#endif
     } else {
       {
         const int vo = PB::voff(t, kx);
@@ -1134,7 +1114,11 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
                            target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,
                            pd.plane_slot, pd.plane_spares, pd.spare_base, pd.rc_pending, pd.rc_cache,
                            *pd.walk_planes);
-      } else if (HBX_ROWINV_LEAN_ON && pd.plane_mode == kPlanesOff && !field_out && !pd.rc_pending) {
+      } else if (pd.plane_mode == kPlanesOff && !field_out && !pd.rc_pending) {
+        // (r06) the plain FFT-mode launch (the headline): its own instantiation without the plane
+        // cache / field / reconcile / walk code -- 1,687 instead of 4,988 instructions; same
+        // arithmetic and bits, k_rowinv 1.465-1.515 -> 1.444-1.457 ms alternated on one box
+        // (profiles/r06/rowinv_lean_ab_r06e.txt)
         hipLaunchKernelGGL((k_rowinv_d<R, false, true>), dim3(blocks), dim3(256), 0, st, jobs, pd.ws_b,
                            target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
                            target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool,

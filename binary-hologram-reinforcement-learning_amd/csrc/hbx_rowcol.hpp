@@ -155,29 +155,4 @@ __device__ __forceinline__ void col2_stage_store(const float2* scratch, __amdgpu
   }
 }
 
-// (r06 experiment) the same stores with the per-chunk-round offset folded into a buffer descriptor
-// per round (SALU: the base address moves) instead of a VALU add per store: voffset is the one
-// lane VGPR, soffset the literal 0
-template <int R, int N = R * R>
-__device__ __forceinline__ void col2_stage_store_p(const float2* scratch, uint64_t bplane_sgpr, int st) {
-  constexpr int TL = 256 / R, CH = N * TL / 2;
-  static_assert(CH % 256 == 0, "whole chunk rounds");
-  const int tid = threadIdx.x, sp = tid % (TL / 2);
-  const int band0 = tid / (8 * TL), r = (tid / (TL / 2)) % 16;
-  const int y0 = band0 * 16 + r;
-  const float2* lo_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp) + col2_pos<R>(sp, y0);
-  const float2* hi_r = col2_region<R>(const_cast<float2*>(scratch), 2 * sp + 1) + col2_pos<R>(sp, y0);
-  const int voff = (band0 * 16 * N + r * TL + 2 * sp) * 8;
-#pragma unroll
-  for (int i = 0; i < CH / 256; ++i) {
-    const float2 lo = lo_r[(32 / TL) * 16 * i];
-    const float2 hi = hi_r[(32 / TL) * 16 * i];
-    const u32x4 o = {__float_as_uint(lo.x), __float_as_uint(lo.y), __float_as_uint(hi.x), __float_as_uint(hi.y)};
-    const uint64_t a = bplane_sgpr + ((uint64_t)st * 16 * TL + (uint64_t)i * (32 / TL) * 16 * N) * 8;
-    const __amdgpu_buffer_rsrc_t ri =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), (short)0, (int)(2u << 20), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(o, ri, voff, 0, kBufNT);
-  }
-}
-
 }  // namespace hbx
