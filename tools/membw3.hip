@@ -318,17 +318,67 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_rows(const float2* __restrict
   if (acc == 12345.f) out[0] = acc;
 }
 
+// (r06) channel de-aliasing: pad every B band (128 KB at TL = 8) by PADB float2 and every A panel
+// (32 KB) by PADA float2, so the 1-KB pieces of one block (B: 64 bands at the band stride; A: 4
+// panels per 32 rows) stop landing on the same HBM channel
+template <int PADB, int PADA>
+__global__ __launch_bounds__(256, 2) void k_col2_pad(const float2* __restrict__ A, float2* __restrict__ B) {
+  constexpr int TL = 8, NT = 256, ITER = 4, LB = (N / 2) / (TL * ITER), KSTEP = LB * TL;
+  constexpr size_t PLA = (size_t)(N / 2) * N + (size_t)(N / 8) * PADA, PLB = (size_t)N * N + (size_t)(N / 16) * PADB;
+  __shared__ __attribute__((aligned(16))) float2 tile[N * TL];
+  const int grp = threadIdx.x / R, t = threadIdx.x % R;
+  int bid = blockIdx.x;
+  const int lb = bid % LB;
+  bid /= LB;
+  const float2* a = A + (size_t)bid * PLA;
+  float2* b = B + (size_t)bid * PLB;
+  for (int it = 0; it < ITER; ++it) {
+    const int kx0 = lb * TL + it * KSTEP;
+    const int kx = kx0 + grp;
+    float2 v[R];
+#pragma unroll
+    for (int jj = 0; jj < R; ++jj) {
+      const int y = t + R * jj;
+      v[jj] = a[pan_at<8, N / 2>(kx, y) + (size_t)(y / 8) * PADA];
+    }
+    for (int set = 0; set < 2; ++set) {
+      lds_barrier();
+#pragma unroll
+      for (int k2 = 0; k2 < R; ++k2) {
+        const int y = t + R * k2;
+        const int band = y / 16, r = y % 16;
+        tile[band * 16 * TL + r * TL + (grp ^ (r & (TL - 1)))] = v[k2];
+      }
+      lds_barrier();
+      constexpr int CH = N * TL / 2;
+#pragma unroll
+      for (int i = 0; i < CH / NT; ++i) {
+        const int c = threadIdx.x + NT * i;
+        const int band = c / (8 * TL), r = (c / (TL / 2)) % 16, lp = (c % (TL / 2)) * 2;
+        const float2 w0 = tile[band * 16 * TL + r * TL + (lp ^ (r & (TL - 1)))];
+        const float2 w1 = tile[band * 16 * TL + r * TL + ((lp + 1) ^ (r & (TL - 1)))];
+        const int line0 = set == 0 ? kx0 : (kx0 == 0 ? N - TL : N - kx0 - TL);
+        *reinterpret_cast<float4*>(b + ((size_t)band * (N / TL) + line0 / TL) * (16 * TL) + (size_t)band * PADB +
+                                   r * TL + lp) = make_float4(w0.x, w0.y, w1.x, w1.y);
+      }
+#pragma unroll
+      for (int jj = 0; jj < R; ++jj) v[jj] = make_float2(v[jj].y, v[jj].x);
+    }
+  }
+}
+
 int main() {
   const int jobs = 128;
   const size_t a_bytes = (size_t)jobs * P * (N / 2) * N * 8;   // 4.29 GB
-  const size_t b_bytes = 2 * a_bytes;                           // 8.59 GB
+  const size_t a_alloc = a_bytes + (size_t)jobs * P * (N / 8) * 64 * 8 + (1 << 20);   // + A panel pads
+  const size_t b_bytes = 2 * a_bytes + (size_t)jobs * P * (N / 16) * 512 * 8 + (1 << 20);   // 8.59 GB + pads
   float2 *A, *B;
   float* o;
-  if (hipMalloc(&A, a_bytes) != hipSuccess || hipMalloc(&B, b_bytes) != hipSuccess || hipMalloc(&o, 64) != hipSuccess) {
+  if (hipMalloc(&A, a_alloc) != hipSuccess || hipMalloc(&B, b_bytes) != hipSuccess || hipMalloc(&o, 64) != hipSuccess) {
     printf("alloc failed\n");
     return 1;
   }
-  (void)hipMemset(A, 0, a_bytes);
+  (void)hipMemset(A, 0, a_alloc);
   (void)hipMemset(B, 0, b_bytes);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
@@ -358,24 +408,17 @@ int main() {
        [&] { hipLaunchKernelGGL(k_r1w2_flat, g16, 256, 0, 0, (const float4*)A, (float4*)B, n16); });
   const unsigned gcol = jobs * P * 16;
   for (int rep = 0; rep < 2; ++rep) {
-    time("col2_A8_B16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_direct<16>), gcol, 256, 0, 0, A, B); });
-    time("col2_A8_B8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_direct<8>), gcol, 256, 0, 0, A, B); });
-    time("col2_A8_B8_lds", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_lds<8>), gcol, 256, 0, 0, A, B); });
-    time("col2_A8_B16_lds", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_lds<16>), gcol, 256, 0, 0, A, B); });
-    time("rowinv_pan8", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_rows<8>), jobs * (N / 8), 256, 0, 0, B, o); });
-    time("rowinv_pan16", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_rows<16>), jobs * (N / 8), 256, 0, 0, B, o); });
     time("col2_T8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8>), gcol, 256, 0, 0, A, B); });
-    time("col2_T16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<16>), gcol / 2, 512, 0, 0, A, B); });
-    // (r06) A in taller panels: k_col2's line reads become 128-B / 256-B pieces
-    time("col2_T8_A16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8, 16>), gcol, 256, 0, 0, A, B); });
-    time("col2_T8_A32", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<8, 32>), gcol, 256, 0, 0, A, B); });
-    time("col2_T16_A16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_tiled<16, 16>), gcol / 2, 512, 0, 0, A, B); });
-    time("col2_T8_direct8", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<false>), gcol, 256, 0, 0, A, B); });
-    time("col2_T8_swap16", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_t8_direct<true>), gcol, 256, 0, 0, A, B); });
-    time("rowinv_direct_pan16", (double)b_bytes, [&] { hipLaunchKernelGGL(k_rowinv_direct_pan16, jobs * (N / 8), 256, 0, 0, B, o); });
-    time("rowinv_direct_t8", (double)b_bytes, [&] { hipLaunchKernelGGL(k_rowinv_direct_t8, jobs * (N / 8), 256, 0, 0, B, o); });
-    time("rowinv_T8", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_tiled<8>), jobs * (N / 8), 256, 0, 0, B, o); });
-    time("rowinv_T16", (double)b_bytes, [&] { hipLaunchKernelGGL((k_rowinv_tiled<16>), jobs * (N / 8), 256, 0, 0, B, o); });
+    time("col2_pad_0_0", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<0, 0>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_128_0", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<128, 0>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_256_0", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<256, 0>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_512_0", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<512, 0>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_0_32", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<0, 32>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_0_64", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<0, 64>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_128_32", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<128, 32>), gcol, 256, 0, 0, A, B); });
+    time("col2_pad_256_64", 3.0 * a_bytes, [&] { hipLaunchKernelGGL((k_col2_pad<256, 64>), gcol, 256, 0, 0, A, B); });
+    time("flat_r1w2", 3.0 * a_bytes,
+         [&] { hipLaunchKernelGGL(k_r1w2_flat, g16, 256, 0, 0, (const float4*)A, (float4*)B, n16); });
   }
   return 0;
 }
