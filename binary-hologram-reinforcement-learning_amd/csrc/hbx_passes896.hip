@@ -348,6 +348,7 @@ __global__ __launch_bounds__(256, 2) void k_col896(const JobDesc* __restrict__ j
 // ---------------------------------------------------------------------------
 constexpr bool kInvScalar = false;   // packed DFTs (one line live)
 
+template <bool LEAN>
 __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict__ jobs,
                                                       const float2* __restrict__ ws_b,
                                                       const float* __restrict__ target,
@@ -360,6 +361,10 @@ __global__ __launch_bounds__(256, 2) void k_rowinv896(const JobDesc* __restrict_
                                                       const int32_t* __restrict__ plane_slot, int plane_spares,
                                                       int spare_base) {
   constexpr int TL = 8;                           // slots per tile (1-KB tiles, as N = 1024)
+  if constexpr (LEAN) {   // (r06) the plain FFT-mode launch: no plane-cache / field code (as k_rowinv_d)
+    plane_mode = kPlanesOff;
+    field_out = nullptr;
+  }
   __shared__ float2 tw[kN];
   __shared__ float2 scratch[kSCR];
   __shared__ double red[kGPB][3];
@@ -515,10 +520,21 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
                      pd.ws_b, pd.htab, pd.tw, P, pair);
   if (tm) tm->end(1, n_jobs, st);
   if (tm) tm->begin(2, st);
-  hipLaunchKernelGGL(k_rowinv896, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
-                     target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
-                     target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot,
-                     pd.plane_spares, pd.spare_base);
+#ifdef HBX_ROWINV896_FAT
+  const bool lean = false;
+#else
+  const bool lean = pd.plane_mode == kPlanesOff && !field_out;
+#endif
+  if (lean)
+    hipLaunchKernelGGL(k_rowinv896<true>, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
+                       target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                       target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot,
+                       pd.plane_spares, pd.spare_base);
+  else
+    hipLaunchKernelGGL(k_rowinv896<false>, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
+                       target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
+                       target ? ~(size_t)0 : (size_t)0, pd.inten_by_env, pd.plane_mode, pd.plane_pool, pd.plane_slot,
+                       pd.plane_spares, pd.spare_base);
   if (tm) tm->end(2, n_jobs, st);
   hipLaunchKernelGGL(k_reduce_partials, dim3(n_jobs), dim3(64), 0, st, pd.partial, n_jobs, kRB,
                      pd.job_stats);

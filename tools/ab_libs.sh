@@ -5,7 +5,7 @@ set -o pipefail
 T=$1; REPS=$2; shift 2
 L=binary-hologram-reinforcement-learning_amd/hbx
 mkdir -p gpurun_out/$T
-Q="--steps 20 --warmup 3 --no-psf --no-ppo --no-probe --no-precision --no-obs --dbs-flips 0 --cpu-sample 0 --no-psnr-check --no-planes --no-crop --no-dropin --no-scipy ${AB_EXTRA}"
+Q="${AB_Q:---steps 20 --warmup 3 --no-psf --no-ppo --no-probe --no-precision --no-obs --dbs-flips 0 --cpu-sample 0 --no-psnr-check --no-planes --no-crop --no-dropin --no-scipy}"
 for r in $(seq 1 $REPS); do
   for lib in "$@"; do
     HBX_LIB=$PWD/$L/$lib.so timeout -k 10 300 python bench.py $Q > gpurun_out/$T/${lib}_$r.json 2> gpurun_out/$T/${lib}_$r.err || exit 1
