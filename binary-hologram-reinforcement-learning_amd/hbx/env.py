@@ -148,7 +148,7 @@ class HostObsMirror:
         for k in self.keys:
             shape, dt = self.shapes[k]
             if k == "recon_image":
-                t = torch.empty(shape, dtype=torch.float32, pin_memory=True)
+                t = torch.empty(shape, dtype=torch.float32, pin_memory=self.vec.device.type == "cuda")
                 self._recon_t[s] = t
                 d[k] = t.numpy()
             else:
@@ -236,7 +236,8 @@ class HostObsMirror:
         """A reset-only call: the whole recon_image from the device (blocking)."""
         if "recon_image" in self.keys and self.valid[self.cur]:
             self.queue_recon()
-            torch.cuda.current_stream(self.vec.device).synchronize()
+            if self.vec.device.type == "cuda":
+                torch.cuda.current_stream(self.vec.device).synchronize()
 
     def invalidate(self):
         self.valid = [False, False]
