@@ -178,3 +178,14 @@ def test_shim_binary_check_raises_without_a_sync_in_simulate():
     with pytest.raises(ValueError, match="binary"):   # an earlier call's input, seen at the next call
         tt.simulate(tt.Tensor(torch.from_numpy(good).cuda(), meta=meta), 2e-3)
     tt.check_binary()                            # nothing pending
+
+
+def test_pack_threshold_full_headline_size():
+    """configs[2]'s reset input at full size (24 x 1024 x 1024 f32 per env, 4 envs): pack then
+    unpack equals `pre >= 0.5` bit for bit (a size-independent round trip, on the device)."""
+    import hbx
+    g = torch.Generator(device="cuda").manual_seed(17)
+    pre = torch.rand((4, 24, 1024, 1024), generator=g, device="cuda")
+    bits = hbx.pack_mask(pre, threshold=0.5)
+    assert bits.shape == (4, 24, 1024, 16)
+    assert torch.equal(hbx.unpack_bits(bits, 1024), (pre >= 0.5).to(torch.int8))
