@@ -53,36 +53,78 @@ _PARAM_ATTRS = {"max_steps": ("max_steps", int), "T_PSNR": ("t_psnr", float), "T
 class LazyObs(dict):
     """Dict observation kept on the GPU whose values become numpy arrays on first
     access (cached): an SB3 rollout buffer that reads every key pays one device ->
-    host copy per key.  ``.device(key)`` returns the device tensor without a copy.
+    host copy per key.  ``.device(key)`` returns the key as a device tensor.
 
     The env's observations are VIEWS of buffers the next step rewrites (ABI v8).  A key
     first read after the next env.step() must still show this step's data (SB3 assigns
-    self._last_obs into its rollout buffer after the following step), so the
-    env snapshots (device clone, queued on the stream before its launches) the keys of its
-    last LazyObs that are still unread AND that the next launch rewrites: state_record /
-    state / recon_image before a step, every key before a reset.  A consumer that reads
-    every key before stepping pays no snapshot; one that reads none pays a device copy of
-    the step-mutable keys only (target / pre_model change at resets alone)."""
+    self._last_obs into its rollout buffer after the following step), so before
+    the env launches work that rewrites a buffer, the LazyObs objects that still hold it unread
+    keep their values (r06, VERDICT r05 #5 -- no device copy on SB3's host-action step):
+
+    * state / state_record change by one byte per env per step (env.py:164-165): the LazyObs
+      keeps an UNDO log of the later steps' (pixel, accepted) on the host and applies it in
+      reverse to the live buffer when the key is finally read (int8 wraps like numpy's);
+    * recon_image at one colour group is rewritten whole by every step: the env steps into its
+      second recon buffer (ping-pong) and the LazyObs keeps the first;
+    * anything else -- a reset, a device-tensor or graph-replayed step, recon at G > 1, an undo
+      log past `UNDO_MAX` steps -- takes the r05 path: a device clone (queued before the
+      launch), or for an undo-tracked key its materialised host copy."""
+
+    UNDO_MAX = 16
 
     def __init__(self, tensors: dict):
         super().__init__()
         self._t = dict(tensors)
         self._owned = set()
+        self._tracked = set()        # keys restored from the live buffer + the undo log on read
+        self._undo = []              # (env idx, channel, row, col, accepted) per later step
         for k in self._t:
             dict.__setitem__(self, k, None)
 
+    def _unread(self, k):
+        return k in self._t and k not in self._owned and dict.__getitem__(self, k) is None
+
     def _snapshot(self, keys):
-        """Own a device copy of every listed key not read yet (the env calls this before it
-        launches work that rewrites those buffers)."""
+        """Own a copy of every listed key not read yet (the env calls this before it launches
+        work that rewrites those buffers): undo-tracked keys are materialised on the host, the
+        others cloned on the device."""
         for k in keys:
-            if k in self._t and k not in self._owned and dict.__getitem__(self, k) is None:
+            if k in self._tracked:
+                self[k]
+            elif self._unread(k):
                 self._t[k] = self._t[k].clone()
                 self._owned.add(k)
+
+    def _track(self, keys) -> bool:
+        """Keep the listed unread one-byte-per-step keys by undo log instead of a copy."""
+        for k in keys:
+            if self._unread(k):
+                self._tracked.add(k)
+        return bool(self._tracked)
+
+    def _record(self, op):
+        """The env's step `op` = (b, c, r, col, accepted) arrays, applied to the live buffers."""
+        if not self._tracked:
+            return
+        self._undo.append(op)
+        if len(self._undo) > self.UNDO_MAX:      # bound the log: materialise
+            for k in list(self._tracked):
+                self[k]
 
     def __getitem__(self, k):
         v = dict.__getitem__(self, k)
         if v is None:
             v = self._t[k].detach().cpu().numpy()
+            if k in self._tracked:
+                for b, c, r, col, acc in reversed(self._undo):   # newest step first
+                    if k == "state_record":
+                        v[b, 0, c, r, col] -= np.int8(1)
+                    else:
+                        v[b, 0, c, r, col] ^= acc
+                self._tracked.discard(k)
+                self._owned.add(k)
+                if not self._tracked:
+                    self._undo = []
             dict.__setitem__(self, k, v)
         return v
 
@@ -100,7 +142,9 @@ class LazyObs(dict):
         as the caller keeps it: a key still aliasing an env buffer the next step rewrites is
         snapshotted (one device copy) first, so the tensor handed out never changes under the
         caller."""
-        if k not in self._owned and dict.__getitem__(self, k) is None:
+        if k in self._tracked:
+            self._t[k] = torch.from_numpy(self[k]).to(self._t[k].device)
+        elif self._unread(k):
             self._t[k] = self._t[k].clone()
             self._owned.add(k)
         return self._t[k]
@@ -476,7 +520,9 @@ class HologramVecEnv(_VecEnvBase):
         self._fast_ids = None
         self._settle_args = None
         self._obs_views = None
-        self._lazy_ref = None      # the last LazyObs handed out (obs_format="lazy")
+        self._lazy_refs = []       # the LazyObs handed out that may still alias live buffers (lazy)
+        self._lazy_track = False   # this step's deltas are known on the host (undo logs, r06)
+        self._recon_swapped = False
         self._in_step = False
         # obs_format="numpy": host mirrors updated by the reference's rules, recon the only D2H
         self._mirror = HostObsMirror(self) if obs_format == "numpy" else None
@@ -505,14 +551,83 @@ class HologramVecEnv(_VecEnvBase):
             st.pre_model[i].copy_(pre)
         self.episode_count += 1
 
+    def _lazy_alive(self):
+        """The LazyObs still alive that hold an unread step-mutable key or an undo log."""
+        alive, refs = [], []
+        for r in self._lazy_refs:
+            lz = r()
+            if lz is not None and (lz._tracked or any(lz._unread(k) for k in OBS_KEYS)):
+                alive.append(lz)
+                refs.append(r)
+        self._lazy_refs = refs
+        return alive
+
+    def _recon_pingpong_ok(self) -> bool:
+        """recon_image rewritten whole by every step (one colour group, ABI v12) and its pointer
+        read per launch (no captured graph): the step can write into the second buffer."""
+        return (self.cfg.groups == 1 and self.mode != "psf" and not self.use_graph
+                and self.state.recon is not None)
+
+    def _swap_recon(self, alive) -> bool:
+        st = self.state
+        live = st.recon.data_ptr()
+        if not any(lz._unread("recon_image") and lz._t["recon_image"].data_ptr() == live for lz in alive):
+            return False
+        if getattr(st, "recon_alt", None) is None:
+            st.recon_alt = torch.empty_like(st.recon)
+        alt = st.recon_alt.data_ptr()
+        for lz in alive:                 # a LazyObs two steps old still holding the other buffer
+            if lz._unread("recon_image") and lz._t["recon_image"].data_ptr() == alt:
+                lz._snapshot(("recon_image",))
+        st.recon, st.recon_alt = st.recon_alt, st.recon
+        st.bufs.recon = st.recon.data_ptr()
+        self._obs_views = None
+        return True
+
     def _before_launch(self, keys):
-        """The last LazyObs snapshots its unread `keys` before work that rewrites them is queued."""
-        if self._lazy_ref is not None:
-            lz = self._lazy_ref()
-            if lz is None:
-                self._lazy_ref = None
+        """Before work that rewrites `keys` is queued, every LazyObs still holding one of them
+        unread keeps its values (class LazyObs): on SB3's host-action step (self._lazy_track)
+        state / state_record by undo log and recon_image (one colour group) by the recon
+        ping-pong; otherwise by a snapshot."""
+        if not self._lazy_refs:
+            return
+        alive = self._lazy_alive()
+        if not alive:
+            return
+        track = self._lazy_track and set(keys) == set(STEP_OBS_KEYS)
+        swapped = False
+        if track and self._recon_pingpong_ok():
+            swapped = self._swap_recon(alive)
+        self._recon_swapped = swapped
+        for lz in alive:
+            if track:
+                lz._track(("state", "state_record"))
+                lz._snapshot(tuple(k for k in keys if k not in ("state", "state_record")
+                                   and not (swapped and k == "recon_image")))
             else:
                 lz._snapshot(keys)
+
+    def _lazy_record(self, actions: np.ndarray, accepted: np.ndarray, envs: Optional[np.ndarray] = None):
+        """This step's one-byte changes (of `envs`, default all) into the undo logs of the LazyObs
+        it rewrote."""
+        c = self.cfg
+        b = np.arange(self.num_envs) if envs is None else envs
+        ch, pix = np.divmod(actions.astype(np.int64)[b], c.height * c.width)
+        r, col = np.divmod(pix, c.width)
+        op = (b, ch, r, col, (accepted[b] != 0).astype(np.int8))
+        for lz in self._lazy_alive():
+            lz._record(op)
+
+    def _lazy_error(self, actions: np.ndarray, accepted: np.ndarray):
+        """An out-of-range action: that env's step was a no-op (nothing flipped, recorded or
+        written), the others stepped.  The undo logs get the valid envs' changes only, and the
+        swapped-in recon buffer gets the offending envs' previous rows back."""
+        bad = (actions < 0) | (actions >= self.num_pixels)
+        alt = getattr(self.state, "recon_alt", None)
+        if bad.any() and getattr(self, "_recon_swapped", False) and alt is not None:
+            idx = torch.as_tensor(np.nonzero(bad)[0], device=self.device)
+            self.state.recon[idx] = alt[idx]
+        self._lazy_record(actions, accepted, np.nonzero(~bad)[0])
 
     def reset_envs(self, env_ids: Sequence[int]):
         ids = [int(i) for i in env_ids]
@@ -563,7 +678,7 @@ class HologramVecEnv(_VecEnvBase):
             return _to_numpy(obs)
         if self.obs_format == "lazy":
             lz = LazyObs(obs)
-            self._lazy_ref = weakref.ref(lz)
+            self._lazy_refs.append(weakref.ref(lz))
             return lz
         return obs
 
@@ -777,6 +892,10 @@ class HologramVecEnv(_VecEnvBase):
         a_host = None
         if m is not None:
             a_host = self._act_np.copy() if hostpath else self._actions_host(actions)
+        # lazy format: the step's deltas go into the undo logs of the LazyObs it would rewrite
+        self._lazy_track = hostpath and self.obs_format == "lazy" and bool(self._lazy_refs)
+        if self._lazy_track and a_host is None:
+            a_host = self._act_np.copy()
         if hostpath:
             if self.use_graph and self.device.type == "cuda":
                 self._graph_fast()
@@ -805,12 +924,17 @@ class HologramVecEnv(_VecEnvBase):
             # a blocking wait: spinning on ev.query() measured no faster (0.3303 vs 0.3276 ms per
             # 256x8 step, profiles/archive/r04/step_host_r04g.txt) and would burn a core
             self._readback.synchronize()
+        lazy_track, self._lazy_track = self._lazy_track, False
         if self._h_err[0]:
             if m is not None:
                 m.invalidate()
+            if lazy_track:
+                self._lazy_error(a_host, self._host_np[16 * n:17 * n])
             self.state.check_error()                      # clears the word and raises
         if m is not None:
             m.step_delta(a_host, self._host_np[16 * n:17 * n])
+        if lazy_track:
+            self._lazy_record(a_host, self._host_np[16 * n:17 * n])
         r = self._h_rew.copy() if self.obs_format == "torch" else self._h_rew.astype(np.float32)
         dones = np.logical_or(self._h_term, self._h_trunc)   # the kernels write 0 / 1
         if self.auto_reset and dones.any():

@@ -519,3 +519,50 @@ def test_graph_lazy_obs_snapshot_not_recorded():
     assert lazy._graph_h is not None
     eager.close()
     lazy.close()
+
+
+@pytest.mark.parametrize("rgb", [False, True])
+def test_lazy_obs_undo_and_recon_pingpong_equal_torch_obs(rgb):
+    """obs_format="lazy" (r06): on SB3's host-action step an unread state / state_record is kept by
+    an undo log and recon_image (one colour group) by the recon ping-pong, no device copy.  Against
+    a torch-format twin: every LazyObs read 0, 1, 2 or 5 steps after it was returned shows its own
+    step's values, across rollbacks, auto-resets and an out-of-range action; RGB (G = 3) takes the
+    recon clone."""
+    import hbx
+    from hbx.env import HologramVecEnv, OBS_KEYS
+    cfg = hbx.OpticsConfig(64, 64, 3, 2, hbx.plan.WL_RGB) if rgb else hbx.mono_config(256)
+    N = cfg.height
+    B = 4
+    g = torch.Generator(device="cuda").manual_seed(61)
+    pres = [torch.rand((cfg.channels, N, N), generator=g, device="cuda") for _ in range(B)]
+    tgts = [torch.rand((cfg.groups, N, N), generator=g, device="cuda") for _ in range(B)]
+    kw = dict(pre_model_source=lambda i: pres[i], auto_reset=True, max_steps=23, obs_keys=OBS_KEYS)
+    ref = HologramVecEnv(cfg, B, lambda i: tgts[i], **kw)
+    lazy = HologramVecEnv(cfg, B, lambda i: tgts[i], obs_format="lazy", **kw)
+    ref.reset()
+    lazy.reset()
+    acts = torch.randint(0, cfg.channels * N * N, (90, B), generator=g, device="cuda").cpu().numpy()
+    held = []                                   # (LazyObs, its step's values, read after k steps)
+    swaps = 0
+    for s in range(90):
+        if s == 45:                             # an out-of-range action: ValueError, other envs step
+            bad = acts[s].copy()
+            bad[1] = cfg.channels * N * N
+            for e in (ref, lazy):
+                with pytest.raises(ValueError):
+                    e.step(bad)
+            continue
+        o1, _, d1, _ = ref.step(acts[s])
+        live = lazy.state.recon.data_ptr()
+        o2, _, d2, _ = lazy.step(acts[s])
+        swaps += int(lazy.state.recon.data_ptr() != live)
+        assert np.array_equal(d1, d2), s
+        held.append((o2, {k: o1[k].cpu().numpy().copy() for k in OBS_KEYS}, s, (0, 1, 2, 5)[s % 4]))
+        for lz, want, s0, k in list(held):
+            if s - s0 == k:
+                for key in OBS_KEYS:
+                    assert np.array_equal(lz[key], want[key]), (s0, s, key)
+                held.remove((lz, want, s0, k))
+    assert not rgb and swaps > 0 or rgb and swaps == 0
+    ref.close()
+    lazy.close()

@@ -109,3 +109,39 @@ def test_mirror_int8_record_wraps_like_numpy():
         m.step_delta(np.array([5]), np.array([0], np.uint8))
     assert m.obs()["state_record"][0, 0, 0, 0, 5] == np.int8(300 - 256)
     _check(m.obs(), vec.want(), "wrap")
+
+
+def test_lazyobs_undo_log_restores_older_values():
+    """LazyObs (obs_format="lazy", r06): an unread state / state_record key is kept by an undo log
+    of the later steps' one-byte changes instead of a device copy; reading it after k more steps
+    gives the values it was created with (int8 record wrap included); past UNDO_MAX steps the key
+    is materialised."""
+    from hbx.env import LazyObs
+    rng = np.random.default_rng(4)
+    B, CH, N = 3, 2, 8
+    rec = torch.from_numpy(rng.integers(-128, 128, (B, CH, N, N)).astype(np.int8))
+    rec[0, 1, 2, 3] = 127                                # wraps on the next +1
+    st = torch.from_numpy((rng.random((B, CH, N, N)) < 0.5).astype(np.int8))
+    want = {"state_record": rec.numpy()[:, None].copy(), "state": st.numpy()[:, None].copy()}
+    lz = LazyObs({"state_record": rec.unsqueeze(1), "state": st.unsqueeze(1)})
+    assert lz._track(("state", "state_record"))
+    for step in range(LazyObs.UNDO_MAX):
+        b = np.arange(B)
+        c, r, col = rng.integers(0, CH, B), rng.integers(0, N, B), rng.integers(0, N, B)
+        if step == 0:
+            c[0], r[0], col[0] = 1, 2, 3
+        acc = (rng.random(B) < 0.5).astype(np.int8)
+        for i in range(B):                               # the "device" step
+            rec[i, c[i], r[i], col[i]] += 1
+            st[i, c[i], r[i], col[i]] ^= int(acc[i])
+        lz._record((b, c, r, col, acc))
+    assert np.array_equal(lz["state"], want["state"])
+    assert np.array_equal(lz["state_record"], want["state_record"])
+    lz2 = LazyObs({"state": st.unsqueeze(1)})
+    lz2._track(("state",))
+    snap = st.numpy()[:, None].copy()
+    for _ in range(LazyObs.UNDO_MAX + 1):                # one past the bound: materialised then
+        st[:, 0, 0, 0] ^= 1
+        lz2._record((np.arange(B), np.zeros(B, np.int64), np.zeros(B, np.int64), np.zeros(B, np.int64),
+                     np.ones(B, np.int8)))
+    assert not lz2._tracked and np.array_equal(lz2["state"], snap)
