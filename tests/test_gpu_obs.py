@@ -558,11 +558,14 @@ def test_lazy_obs_undo_and_recon_pingpong_equal_torch_obs(rgb):
         swaps += int(lazy.state.recon.data_ptr() != live)
         assert np.array_equal(d1, d2), s
         held.append((o2, {k: o1[k].cpu().numpy().copy() for k in OBS_KEYS}, s, (0, 1, 2, 5)[s % 4]))
-        for lz, want, s0, k in list(held):
+        keep = []
+        for lz, want, s0, k in held:
             if s - s0 == k:
                 for key in OBS_KEYS:
                     assert np.array_equal(lz[key], want[key]), (s0, s, key)
-                held.remove((lz, want, s0, k))
+            else:
+                keep.append((lz, want, s0, k))
+        held = keep
     assert not rgb and swaps > 0 or rgb and swaps == 0
     ref.close()
     lazy.close()

@@ -23,6 +23,17 @@ def main():
     if "reset" in what:
         out["reset_1024x24"] = bench.reset_cost(rgb_config(1024))
         print(json.dumps(out), flush=True)
+    if "lazy" in what:
+        mono = mono_config(256)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        pres = [torch.rand((8, 256, 256), generator=g, device="cuda") for _ in range(128)]
+        tgts = [torch.rand((1, 256, 256), generator=g, device="cuda") for _ in range(128)]
+        for fmt in ("torch", "lazy"):
+            r = bench.vecenv_step_obs(mono, 128, 240, 5, lambda i: tgts[i], lambda i: pres[i], 0.33, 12,
+                                      obs_format=fmt)
+            out[f"vecenv_step_obs_{fmt}"] = {k: r[k] for k in ("ms_per_step", "pure_device_step_ms",
+                                                              "overhead_vs_pure_device_step")}
+        print(json.dumps(out), flush=True)
     if "numpy" in what:
         mono = mono_config(256)
         g = torch.Generator(device="cuda").manual_seed(3)
