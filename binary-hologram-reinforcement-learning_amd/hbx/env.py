@@ -78,6 +78,8 @@ class LazyObs(dict):
         self._owned = set()
         self._tracked = set()        # keys restored from the live buffer + the undo log on read
         self._undo = []              # (env idx, channel, row, col, accepted) per later step
+        rc = self._t.get("recon_image")
+        self._recon_ptr = None if rc is None else rc.data_ptr()   # the env buffer it aliases
         for k in self._t:
             dict.__setitem__(self, k, None)
 
@@ -523,6 +525,7 @@ class HologramVecEnv(_VecEnvBase):
         self._lazy_refs = []       # the LazyObs handed out that may still alias live buffers (lazy)
         self._lazy_track = False   # this step's deltas are known on the host (undo logs, r06)
         self._recon_swapped = False
+        self._alive_step = []
         self._in_step = False
         # obs_format="numpy": host mirrors updated by the reference's rules, recon the only D2H
         self._mirror = HostObsMirror(self) if obs_format == "numpy" else None
@@ -570,14 +573,14 @@ class HologramVecEnv(_VecEnvBase):
 
     def _swap_recon(self, alive) -> bool:
         st = self.state
-        live = st.recon.data_ptr()
-        if not any(lz._unread("recon_image") and lz._t["recon_image"].data_ptr() == live for lz in alive):
+        live = st.bufs.recon
+        if not any(lz._recon_ptr == live and lz._unread("recon_image") for lz in alive):
             return False
         if getattr(st, "recon_alt", None) is None:
             st.recon_alt = torch.empty_like(st.recon)
         alt = st.recon_alt.data_ptr()
         for lz in alive:                 # a LazyObs two steps old still holding the other buffer
-            if lz._unread("recon_image") and lz._t["recon_image"].data_ptr() == alt:
+            if lz._recon_ptr == alt and lz._unread("recon_image"):
                 lz._snapshot(("recon_image",))
         st.recon, st.recon_alt = st.recon_alt, st.recon
         st.bufs.recon = st.recon.data_ptr()
@@ -589,9 +592,11 @@ class HologramVecEnv(_VecEnvBase):
         unread keeps its values (class LazyObs): on SB3's host-action step (self._lazy_track)
         state / state_record by undo log and recon_image (one colour group) by the recon
         ping-pong; otherwise by a snapshot."""
+        self._alive_step = []
         if not self._lazy_refs:
             return
         alive = self._lazy_alive()
+        self._alive_step = alive         # the LazyObs this launch rewrites (their undo logs follow)
         if not alive:
             return
         track = self._lazy_track and set(keys) == set(STEP_OBS_KEYS)
@@ -607,15 +612,21 @@ class HologramVecEnv(_VecEnvBase):
             else:
                 lz._snapshot(keys)
 
-    def _lazy_record(self, actions: np.ndarray, accepted: np.ndarray, envs: Optional[np.ndarray] = None):
-        """This step's one-byte changes (of `envs`, default all) into the undo logs of the LazyObs
-        it rewrote."""
+    def _lazy_decode(self, actions: np.ndarray, envs: Optional[np.ndarray] = None):
+        """(env, channel, row, col) of this step's pixels -- computed while the step runs."""
         c = self.cfg
         b = np.arange(self.num_envs) if envs is None else envs
         ch, pix = np.divmod(actions.astype(np.int64)[b], c.height * c.width)
         r, col = np.divmod(pix, c.width)
+        return b, ch, r, col
+
+    def _lazy_record(self, actions: np.ndarray, accepted: np.ndarray, envs: Optional[np.ndarray] = None,
+                     decoded=None):
+        """This step's one-byte changes (of `envs`, default all) into the undo logs of the LazyObs
+        it rewrote."""
+        b, ch, r, col = decoded if decoded is not None else self._lazy_decode(actions, envs)
         op = (b, ch, r, col, (accepted[b] != 0).astype(np.int8))
-        for lz in self._lazy_alive():
+        for lz in (self._alive_step if decoded is not None else self._lazy_alive()):
             lz._record(op)
 
     def _lazy_error(self, actions: np.ndarray, accepted: np.ndarray):
@@ -920,6 +931,7 @@ class HologramVecEnv(_VecEnvBase):
                 self._settle()                    # (ABI v12: nothing is pending at one group)
         obs = self.observe(stepped=True)
         infos = [{} for _ in range(self.num_envs)]
+        lazy_dec = self._lazy_decode(a_host) if self._lazy_track else None
         if self._readback is not None:
             # a blocking wait: spinning on ev.query() measured no faster (0.3303 vs 0.3276 ms per
             # 256x8 step, profiles/archive/r04/step_host_r04g.txt) and would burn a core
@@ -934,7 +946,7 @@ class HologramVecEnv(_VecEnvBase):
         if m is not None:
             m.step_delta(a_host, self._host_np[16 * n:17 * n])
         if lazy_track:
-            self._lazy_record(a_host, self._host_np[16 * n:17 * n])
+            self._lazy_record(a_host, self._host_np[16 * n:17 * n], decoded=lazy_dec)
         r = self._h_rew.copy() if self.obs_format == "torch" else self._h_rew.astype(np.float32)
         dones = np.logical_or(self._h_term, self._h_trunc)   # the kernels write 0 / 1
         if self.auto_reset and dones.any():
@@ -1064,11 +1076,15 @@ class HologramVecEnv(_VecEnvBase):
         accepted ones; after a reset it is the reset state's.  The views change with the
         next step: a consumer that keeps an observation copies it (SB3's rollout buffers
         do).  `stepped` is accepted for callers of the r02 signature."""
-        if self._obs_views is None:       # the buffers never move: build the views once
+        if self._obs_views is None:       # the buffers never move (but the lazy recon ping-pong)
             st = self.state
-            src = {"state_record": st.record, "state": st.state_bytes, "pre_model": st.pre_model,
-                   "target_image": st.target, "recon_image": st.recon}
-            self._obs_views = {k: src[k].unsqueeze(1) for k in self.obs_keys}
+            key = None if st.recon is None else st.recon.data_ptr()
+            cache = self.__dict__.setdefault("_views_by_recon", {})
+            if key not in cache:
+                src = {"state_record": st.record, "state": st.state_bytes, "pre_model": st.pre_model,
+                       "target_image": st.target, "recon_image": st.recon}
+                cache[key] = {k: src[k].unsqueeze(1) for k in self.obs_keys}
+            self._obs_views = cache[key]
         return dict(self._obs_views)
 
     # -- checkpoint / resume (SURVEY 5: the env state is plain tensors) ---------------
