@@ -196,12 +196,14 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
       }
     }
     pk2 v[R];
+    with_field_kind(va, vb, [&](auto fk) {
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj) {
-      const int w = (R * jj) >> 5;
-      const int sh = ((R * jj) & 31) + t;
-      v[jj] = (pk2){fmaf(vb, (float)((wa[w] >> sh) & 1u), va), fmaf(vb, (float)((wb[w] >> sh) & 1u), va)};
-    }
+      for (int jj = 0; jj < R; ++jj) {
+        const int w = (R * jj) >> 5;
+        const int sh = ((R * jj) & 31) + t;
+        v[jj] = (pk2){bit_value<fk()>(wa[w], sh, va, vb), bit_value<fk()>(wb[w], sh, va, vb)};
+      }
+    });
     if constexpr (RIT > 1) {
       // next rows' words (the last iteration re-reads its own row: no conditional load)
       load_row(it + 1 < RIT ? y + GPB : y);
@@ -332,9 +334,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
       }
     }
     pk2 v[R];
+    with_field_kind(va, vb, [&](auto fk) {
 #pragma unroll
-    for (int jj = 0; jj < R; ++jj)
-      v[jj] = (pk2){fmaf(vb, (float)((ta >> jj) & 1u), va), fmaf(vb, (float)((tb >> jj) & 1u), va)};
+      for (int jj = 0; jj < R; ++jj)
+        v[jj] = (pk2){bit_value<fk()>(ta, jj, va, vb), bit_value<fk()>(tb, jj, va, vb)};
+    });
     if constexpr (RIT > 1) {
       // next rows' words (the last iteration re-reads its own row: no conditional load)
       load_row(it + 1 < RIT ? y + GPB : y);

@@ -145,9 +145,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
       }
     }
     float2 v[32];
+    with_field_kind(va, vb, [&](auto fk) {
 #pragma unroll
-    for (int jj = 0; jj < kL; ++jj)
-      v[jj] = make_float2(fmaf(vb, (float)((ta >> jj) & 1u), va), fmaf(vb, (float)((tb >> jj) & 1u), va));
+      for (int jj = 0; jj < kL; ++jj)
+        v[jj] = make_float2(bit_value<fk()>(ta, jj, va, vb), bit_value<fk()>(tb, jj, va, vb));
+    });
 #pragma unroll
     for (int jj = kL; jj < 32; ++jj) v[jj] = make_float2(0.f, 0.f);
     // next rows' words (the last iteration re-reads its own row: no conditional load)

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "hbx_fft.hpp"
 
 namespace hbx {
@@ -33,6 +35,27 @@ __device__ __forceinline__ int tile_pos(int line, int r) {
     constexpr int SL = ilog2c(GPB / 8);
     return line * GPB + (r ^ ((((line & (R - 1)) >> SR) << SL) & (GPB - 1)));
   }
+}
+
+// Field value of mask bit sh of word w for the row passes: va + vb * bit (hbx_api.hip's field
+// kinds: amplitude 0 / 1, binary phase exp(i pi bit) = +-1).  The two kinds the plans use are
+// built from the bit with two integer ops instead of extract + convert + fma (the same f32
+// values bit for bit: fmaf(1, b, 0) = b, fmaf(-2, b, 1) = +-1.0f = 0x3F800000 with the sign
+// bit b).  r06: k_rowfwd32 1,311 -> ~1,250 VALU and 168 -> 152 VGPRs per row block,
+// 0.874-0.887 -> 0.852-0.873 ms alternated 4x on one box (profiles/r06/rowfwd_bitop_ab_r06o.txt).
+enum { kFieldAmp = 0, kFieldPhase = 1, kFieldAny = 2 };
+template <int FK>
+__device__ __forceinline__ float bit_value(uint32_t w, int sh, float va, float vb) {
+  if constexpr (FK == kFieldAmp) return (float)((w >> sh) & 1u);
+  else if constexpr (FK == kFieldPhase) return __uint_as_float(((w << (31 - sh)) & 0x80000000u) | 0x3F800000u);
+  else return fmaf(vb, (float)((w >> sh) & 1u), va);
+}
+// f(integral_constant<int, FK>) under a uniform branch on the plan's (va, vb)
+template <class F>
+__device__ __forceinline__ void with_field_kind(float va, float vb, F&& f) {
+  if (va == 0.0f && vb == 1.0f) f(std::integral_constant<int, kFieldAmp>{});
+  else if (va == 1.0f && vb == -2.0f) f(std::integral_constant<int, kFieldPhase>{});
+  else f(std::integral_constant<int, kFieldAny>{});
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
