@@ -184,7 +184,10 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   }
   const size_t hrow = (size_t)(N / 2 + 1) * N;
   std::vector<float2> ht((size_t)G * hrow);
-  const double scale = 1.0 / ((double)N * (double)N);  // ifft2 normalisation
+  // ifft2 normalisation, and 1/2: the row passes write 2 A (their Hermitian split drops its
+  // 0.5 factors, r06), the column passes multiply by H / 2 -- powers of two, so every product
+  // and so B are the bits of A x H (hbx_passes.hip, pass 1).  Only the column passes read ht.
+  const double scale = 0.5 / ((double)N * (double)N);
   for (int g = 0; g < G; ++g)
     for (int kx = 0; kx <= N / 2; ++kx) {
       const double fx = fftfreq(kx, N, o->dx);

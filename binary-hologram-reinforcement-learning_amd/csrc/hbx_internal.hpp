@@ -159,7 +159,7 @@ struct PlanDev {
   float va, vb;        // field = va + vb * bit
   float2* tw;          // [N]  W_N^{t k1} at [k1 * R + t]; N = 1024 appends the
                        // whole-wave tables [16][64] W1024^{L k1}, [16][4] W64^{l0 m1}
-  float2* htab;        // [G][N/2 + 1][N]  H(kx, ky) / N^2
+  float2* htab;        // [G][N/2 + 1][N]  H(kx, ky) / (2 N^2): the row passes write 2 A
   float2* ws_a;        // [max_jobs][P][N/2][N]  half spectrum after k_rowfwd (line kx, over y)
   float2* ws_b;        // [max_jobs][P][N][N]    after k_col (line kx, over y)
   double* partial;     // [max_jobs][N / (256/R)][3]

@@ -14,7 +14,8 @@
 //
 //   k_rowfwd  GPB rows of a plane pair per block: bits -> one complex FFT per
 //             row pair (plane a real, plane b imaginary) -> Hermitian split ->
-//             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0) ->
+//             half spectrum kx < N/2 (Nyquist packed in Im of kx = 0), stored doubled:
+//             2 A, the split's 0.5 factors dropped (r06) and folded into htab = H / 2 ->
 //             LDS tile transpose -> A panel y0 / GPB       [HBM: read N^2/8 B, write 4 N^2 B per plane]
 //   k_col2    one lane group per half-spectrum line kx: FFT over y -> x H and
 //             x conj H (H is even in fx and ky) -> two IFFTs -> B lines kx
@@ -52,6 +53,18 @@ __device__ __forceinline__ float2 store_round(float2 v) {
     return make_float2((float)(_Float16)v.x, (float)(_Float16)v.y);
   } else {
     return v;
+  }
+}
+
+// The row passes' A stores: A is stored doubled (2 A, see htab), so the fp16 study rounds 0.5 v to
+// fp16 and doubles it back -- the fp16 value of A itself (fp16 subnormals are not scale-invariant);
+// bf16 shares f32's exponent range, where doubling commutes with rounding.
+template <int SK>
+__device__ __forceinline__ float2 store_round_a(float2 v) {
+  if constexpr (SK == HBX_PRECISION_F16_STORE) {
+    return make_float2(2.0f * (float)(_Float16)(0.5f * v.x), 2.0f * (float)(_Float16)(0.5f * v.y));
+  } else {
+    return store_round<SK>(v);
   }
 }
 
@@ -219,11 +232,11 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
     for (int k2 = 0; k2 < R / 2; ++k2) {
       const float2 z = from_pk(v[k2]);
       const float2 m = mirror_conj<R>(v, k2, t, lane_base);
-      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-      float2 fb = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      float2 fa = make_float2(z.x + m.x, z.y + m.y);       // 2 A (htab holds H / 2)
+      float2 fb = make_float2(z.y - m.y, m.x - z.x);
       if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
-        fa = make_float2(z.x, zny.x);
-        fb = make_float2(z.y, zny.y);
+        fa = make_float2(z.x + z.x, zny.x + zny.x);
+        fb = make_float2(z.y + z.y, zny.y + zny.y);
       }
       const int kx = t + R * k2;
       tile[tile_pos<R, GPB>(kx, grp)] = fa;
@@ -255,8 +268,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
         a = tile[tile_pos<R, GPB>(line, r2)];
         b = tile[tile_pos<R, GPB>(line, r2 + 1)];
       }
-      a = store_round<SK>(a);
-      b = store_round<SK>(b);
+      a = store_round_a<SK>(a);
+      b = store_round_a<SK>(b);
       const int pl = line / (N / 2);
       // panel layout: (line, y0 + r2) of plane pl -> contiguous 16-B chunks of the panel
       st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line - pl * (N / 2), y0 + r2),
@@ -355,11 +368,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
     for (int k2 = 0; k2 < R / 2; ++k2) {
       const float2 z = from_pk(v[k2]);
       const float2 m = mirror_conj_paired(v, k2, t);
-      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-      fb[k2] = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      float2 fa = make_float2(z.x + m.x, z.y + m.y);       // 2 A (htab holds H / 2)
+      fb[k2] = make_float2(z.y - m.y, m.x - z.x);
       if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
-        fa = make_float2(z.x, zny.x);
-        fb[k2] = make_float2(z.y, zny.y);
+        fa = make_float2(z.x + z.x, zny.x + zny.x);
+        fb[k2] = make_float2(z.y + z.y, zny.y + zny.y);
       }
       tile[tile_pos<R, GPB>(k1 + R * k2, grp)] = fa;
     }
@@ -378,8 +391,8 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
         const int c = threadIdx.x + NT * i;
         const int r2 = (c % (GPB / 2)) * 2;
         const int line = c / (GPB / 2);
-        const float2 a = store_round<SK>(tile[tile_pos<R, GPB>(line, r2)]);
-        const float2 b = store_round<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
+        const float2 a = store_round_a<SK>(tile[tile_pos<R, GPB>(line, r2)]);
+        const float2 b = store_round_a<SK>(tile[tile_pos<R, GPB>(line, r2 + 1)]);
         st_stream4(base + (size_t)pl * PLA + LayoutA<R>::at(line, y0 + r2), make_float4(a.x, a.y, b.x, b.y));
       }
     }

@@ -166,11 +166,11 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd896(const JobDesc* __restrict_
     for (int k2 = 0; k2 < 16; ++k2) {
       const float2 z = v[k2];
       const float2 m = mirror_conj896(v, k2, t, lane_base);
-      float2 fa = make_float2(0.5f * (z.x + m.x), 0.5f * (z.y + m.y));
-      fb[k2] = make_float2(0.5f * (z.y - m.y), -0.5f * (z.x - m.x));
+      float2 fa = make_float2(z.x + m.x, z.y + m.y);       // 2 A (htab holds H / 2)
+      fb[k2] = make_float2(z.y - m.y, m.x - z.x);
       if (k2 == 0 && t == 0) {  // DC and Nyquist of a real row are real
-        fa = make_float2(z.x, zny.x);
-        fb[k2] = make_float2(z.y, zny.y);
+        fa = make_float2(z.x + z.x, zny.x + zny.x);
+        fb[k2] = make_float2(z.y + z.y, zny.y + zny.y);
       }
       if (t < kL) tile[tile896_pos(t + kL * k2, grp)] = fa;
     }

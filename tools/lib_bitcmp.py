@@ -3,8 +3,9 @@ by HBX_LIB at import, so each build runs in its own process):
   HBX_LIB=.../libhbx.so         python tools/lib_bitcmp.py dump a.npz
   HBX_LIB=.../libhbx_exp_X.so   python tools/lib_bitcmp.py dump b.npz
   python tools/lib_bitcmp.py cmp a.npz b.npz
-dump: seeded 1024x1024x24 RGB (4 envs) and 256x256x8 mono (8 envs) masks -> group intensities,
-per-channel statistics and PSNR of hbx_propagate."""
+dump: seeded 1024x1024x24 RGB (4 envs), 256x256x8 mono (8 envs), 896 RGB, binary-phase fields and the
+bf16 / fp16 intermediate-storage study -> group intensities, per-channel statistics and PSNR of
+hbx_propagate."""
 import os
 import sys
 
@@ -17,14 +18,21 @@ def dump(path):
     from hbx import pack_bits
     from hbx.plan import Plan, mono_config, rgb_config
     out = {}
-    for name, cfg, B in (("rgb1024", rgb_config(1024), 4), ("mono256", mono_config(256), 8)):
+    from hbx import FIELD_PHASE, PRECISION_BF16_STORE, PRECISION_F16_STORE, PRECISION_F32
+    cases = (("rgb1024", rgb_config(1024), 4, PRECISION_F32), ("mono256", mono_config(256), 8, PRECISION_F32),
+             ("rgb896", rgb_config(896), 2, PRECISION_F32),
+             ("rgb1024ph", rgb_config(1024, field_kind=FIELD_PHASE), 2, PRECISION_F32),
+             ("mono256ph", mono_config(256, field_kind=FIELD_PHASE), 4, PRECISION_F32),
+             ("mono256bf16", mono_config(256), 4, PRECISION_BF16_STORE),
+             ("rgb1024f16", rgb_config(1024), 1, PRECISION_F16_STORE))
+    for name, cfg, B, prec in cases:
         g = torch.Generator(device="cuda").manual_seed(11)
         ch = cfg.groups * cfg.planes
         n = cfg.height
         pre = torch.rand((B, ch, n, n), generator=g, device="cuda")
         tgt = torch.rand((B, cfg.groups, n, n), generator=g, device="cuda")
         mask = pack_bits(pre >= 0.5)
-        plan = Plan(cfg, max_jobs=max(B * cfg.groups, 16))
+        plan = Plan(cfg, max_jobs=max(B * cfg.groups, 16), precision=prec)
         inten, st, ps = plan.propagate(mask, tgt, want_intensity=True)
         torch.cuda.synchronize()
         out[name + "_inten"] = inten.cpu().numpy()
