@@ -73,15 +73,13 @@ class LazyObs(dict):
     UNDO_MAX = 16
 
     def __init__(self, tensors: dict):
-        super().__init__()
+        super().__init__(dict.fromkeys(tensors))   # every key unread (None)
         self._t = dict(tensors)
         self._owned = set()
         self._tracked = set()        # keys restored from the live buffer + the undo log on read
         self._undo = []              # (env idx, channel, row, col, accepted) per later step
         rc = self._t.get("recon_image")
         self._recon_ptr = None if rc is None else rc.data_ptr()   # the env buffer it aliases
-        for k in self._t:
-            dict.__setitem__(self, k, None)
 
     def _unread(self, k):
         return k in self._t and k not in self._owned and dict.__getitem__(self, k) is None
@@ -625,7 +623,9 @@ class HologramVecEnv(_VecEnvBase):
         """This step's one-byte changes (of `envs`, default all) into the undo logs of the LazyObs
         it rewrote."""
         b, ch, r, col = decoded if decoded is not None else self._lazy_decode(actions, envs)
-        op = (b, ch, r, col, (accepted[b] != 0).astype(np.int8))
+        # the kernels write accepted as 0 / 1 bytes: the one copy the log needs (the host row is
+        # rewritten by the next step)
+        op = (b, ch, r, col, (accepted if envs is None else accepted[b]).astype(np.int8))
         for lz in (self._alive_step if decoded is not None else self._lazy_alive()):
             lz._record(op)
 
@@ -932,6 +932,9 @@ class HologramVecEnv(_VecEnvBase):
         obs = self.observe(stepped=True)
         infos = [{} for _ in range(self.num_envs)]
         lazy_dec = self._lazy_decode(a_host) if self._lazy_track else None
+        # lazy format: the returned object is built while the step is in flight too, and
+        # registered (weakref) only once it is known to be the one returned (no auto-reset)
+        early = LazyObs(obs) if self.obs_format == "lazy" and m is None else None
         if self._readback is not None:
             # a blocking wait: spinning on ev.query() measured no faster (0.3303 vs 0.3276 ms per
             # 256x8 step, profiles/archive/r04/step_host_r04g.txt) and would burn a core
@@ -963,6 +966,10 @@ class HologramVecEnv(_VecEnvBase):
                 infos[i]["TimeLimit.truncated"] = bool(tr[i] and not t[i])
             self.reset_envs(done_ids)
             obs = self.observe(stepped=False)
+            early = None
+        if early is not None:
+            self._lazy_refs.append(weakref.ref(early))
+            return early, r, dones, infos
         return self._format(obs), r, dones, infos
 
     def last_step(self) -> dict:
