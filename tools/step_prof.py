@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--format", default="torch")
+    ap.add_argument("--graph", action="store_true", help="HologramVecEnv(graph=True)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -30,7 +31,7 @@ def main():
     tg = [torch.rand((cfg.groups, n, n), generator=g, device="cuda") for _ in range(B)]
     pm = [torch.rand((cfg.channels, n, n), generator=g, device="cuda") for _ in range(B)]
     vec = HologramVecEnv(cfg, B, lambda i: tg[i], pre_model_source=lambda i: pm[i], obs_keys=OBS_KEYS,
-                         obs_format=a.format, auto_reset=True)
+                         obs_format=a.format, auto_reset=True, graph=a.graph)
     vec.reset()
     rng = np.random.default_rng(1)
     acts = rng.integers(0, cfg.channels * n * n, (a.steps + 50, B)).astype(np.int64)
@@ -50,7 +51,7 @@ def main():
     pr.disable()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
-    print(f"format {a.format}: {period:.4f} ms per step without the profiler")
+    print(f"format {a.format} graph {a.graph}: {period:.4f} ms per step without the profiler")
     print(s.getvalue())
 
 
