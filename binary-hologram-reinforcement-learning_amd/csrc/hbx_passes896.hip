@@ -522,11 +522,8 @@ hipError_t run_jobs_896(const PlanDev& pd, const JobDesc* jobs, int n_jobs, cons
                      pd.ws_b, pd.htab, pd.tw, P, pair);
   if (tm) tm->end(1, n_jobs, st);
   if (tm) tm->begin(2, st);
-#ifdef HBX_ROWINV896_FAT
-  const bool lean = false;
-#else
+  // (r06) the plain FFT-mode launch gets the lean instantiation (profiles/r06/rowinv896_lean_ab_r06i.txt)
   const bool lean = pd.plane_mode == kPlanesOff && !field_out;
-#endif
   if (lean)
     hipLaunchKernelGGL(k_rowinv896<true>, dim3((unsigned)n_jobs * kRB), dim3(256), 0, st, jobs, pd.ws_b,
                        target ? target : pd.zero_row, pd.tw, P, pd.G, pd.partial, inten_out, field_out,
