@@ -70,6 +70,8 @@ struct hbx_plan {
   int walk_split = 0;              // HBX_WALK_SPLIT=1: three-launch batches for every K
   int walk_persist = 0;            // HBX_WALK_PERSIST=1: one cooperative launch per walk call
   int32_t* planes_ticket = nullptr;  // hbx_dbs_walk_planes: the fused decision's arrival counter
+  int32_t* walk_ring = nullptr;      // (r06) its candidate-slot ring base (WalkPlanesArgs::ring)
+  uint8_t* walk_phase = nullptr;     // (r06) [max_jobs] what each job slot still needs (::phase)
 };
 
 namespace {
@@ -221,6 +223,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
   // the plane-cache walk's arrival counter (zero between launches; its user resets it): allocated
   // and zeroed here, not on a walk's first call (no blocking memset inside a hot / captured call)
   if (hipMalloc(&p->planes_ticket, 64) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "walk ticket");
+  if (hipMalloc(&p->walk_ring, 64) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "walk ring");
+  if (hipMalloc(&p->walk_phase, (size_t)max_jobs) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "walk phase");
   if (hipMalloc(&p->accept_flag, (size_t)max_jobs * sizeof(int32_t)) != hipSuccess)
     return cleanup(HBX_ERR_NOMEM, "accept_flag");
   if (hipMalloc(&p->err, sizeof(int32_t)) != hipSuccess) return cleanup(HBX_ERR_NOMEM, "err");
@@ -235,6 +239,8 @@ int hbx_plan_create(hbx_plan_t* out, const hbx_optics_t* o, int32_t max_jobs, in
       hipMemset(p->err, 0, sizeof(int32_t)) != hipSuccess ||
       hipMemset(pd.zero_row, 0, (size_t)N * sizeof(float)) != hipSuccess ||
       hipMemset(p->planes_ticket, 0, 64) != hipSuccess ||
+      hipMemset(p->walk_ring, 0, 64) != hipSuccess ||
+      hipMemset(p->walk_phase, 0, (size_t)max_jobs) != hipSuccess ||
       hbx::launch_jobs_full(nullptr, max_jobs / G, G, p->full_jobs, nullptr) != hipSuccess ||
       hipStreamSynchronize(nullptr) != hipSuccess)
     return cleanup(HBX_ERR_HIP, "table upload");
@@ -262,6 +268,8 @@ int hbx_plan_destroy(hbx_plan_t p) {
   if (p->walk_partial) (void)hipFree(p->walk_partial);
   if (p->walk_counter) (void)hipFree(p->walk_counter);
   if (p->planes_ticket) (void)hipFree(p->planes_ticket);
+  if (p->walk_ring) (void)hipFree(p->walk_ring);
+  if (p->walk_phase) (void)hipFree(p->walk_phase);
   if (p->pd.psf_order) (void)hipFree(p->pd.psf_order);
   if (p->pd.zero_row) (void)hipFree(p->pd.zero_row);
   for (void* q : {(void*)p->map_field, (void*)p->map_inten, (void*)p->map_stats, (void*)p->map_q,
@@ -991,6 +999,15 @@ int hbx_dbs_walk_planes_fill(hbx_plan_t p, uint64_t* base_mask, const float* tar
   // in a launch of its own behind each batch (k_walk_planes, decide = 1)
   const bool fused = pd.R != 0;
   pdx.walk_planes = fused ? &wa : nullptr;
+  // (r06) candidates a batch propagated but did not visit keep their job slot, their pair's B and,
+  // when their colour group saw no accept, their partials: the next batch skips those passes for
+  // them (fused decision only; the 896 path decides in its own launch and re-propagates)
+  // (the decision keeps the accepted (group, pair)s as bits < 48 of one word: G * P / 2 <= 48)
+  if (fused && pd.G * pd.P / 2 <= 48 && !std::getenv("HBX_WALK_NO_RETAIN")) {
+    wa.ring = p->walk_ring;
+    wa.phase = p->walk_phase;
+    pdx.walk_phase = p->walk_phase;
+  }
   HBX_HIP(hbx::launch_walk_planes(wa, 0, st));   // this call's first batch of jobs, from the walk state
   for (int b = 0; b < batches; ++b) {
     HBX_HIP(hbx::run_jobs(pdx, p->jobs, K, reinterpret_cast<const uint32_t*>(base_mask), target, nullptr,

@@ -151,6 +151,13 @@ struct WalkPlanesArgs {
   int64_t* fill_count = nullptr;
   int64_t fill_target = 0;
   int64_t fill_tol = 0;
+  // (r06) candidate retention across batches (fused decision only; nullptr = off): the batch's
+  // candidate i sits in job slot (*ring + i) % K, and phase[slot] tells the passes what a slot
+  // still needs -- 0 everything, 1 only k_rowinv_d (its pair's B is still valid), 2 nothing (its
+  // partials and fresh pair are still valid).  Slots are kept by the candidates a batch propagated
+  // but did not visit (hbx_walk_planes.hpp)
+  int32_t* ring = nullptr;
+  uint8_t* phase = nullptr;
 };
 
 struct PlanDev {
@@ -190,6 +197,8 @@ struct PlanDev {
   const int32_t* rc_pending; // [env] nullable
   float* rc_cache;           // [env][G][N][N] the intensity cache
   int skip_reduce = 0;       // 1: leave the per-row-block partials (a caller reduces them itself)
+  const uint8_t* walk_phase = nullptr;           // (r06) per job slot: 0 all passes, 1 k_rowinv_d only,
+                                                 // 2 none (WalkPlanesArgs::phase; nullptr = all)
   const WalkPlanesArgs* walk_planes = nullptr;   // (r05) plane-cache walk batch: the last k_rowinv_d
                                                  // workgroup decides (hbx_walk_planes.hpp)
   // env step at N = 1024 / 256: the first pass decodes the actions itself (no k_jobs_from_actions

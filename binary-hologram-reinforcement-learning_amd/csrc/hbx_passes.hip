@@ -145,7 +145,8 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
                                                    float2* __restrict__ ws_a,
                                                    const float2* __restrict__ tw_glob, int P,
                                                    int CH, float va, float vb, int pair_step,
-                                                   const int64_t* __restrict__ actions, int32_t* err) {
+                                                   const int64_t* __restrict__ actions, int32_t* err,
+                                                   const uint8_t* __restrict__ phase) {
   constexpr int N = R * R;
   constexpr int GPB = NT / R;          // rows per row block
   constexpr int WPR = N / 32;           // 32-bit mask words per row
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(NT, 512 / NT) void k_rowfwd(const JobDesc* jobs,
   const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
   const int j = bid / npair;
   const JobDesc jb = first_pass_job(jobs, actions, err, j, rbw == 0 && bid % npair == 0, (int64_t)N * N, P, CH);
-  if (jb.env < 0) return;  // uniform per block
+  if (jb.env < 0 || (phase && phase[j])) return;  // uniform per block (a walk slot whose A / B are kept)
   const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
   const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
@@ -295,7 +296,8 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
                                                      float2* __restrict__ ws_a,
                                                      const float2* __restrict__ tw_glob, int P, int CH,
                                                      float va, float vb, int pair_step,
-                                                     const int64_t* __restrict__ actions, int32_t* err) {
+                                                     const int64_t* __restrict__ actions, int32_t* err,
+                                                     const uint8_t* __restrict__ phase) {
   constexpr int R = 32, NT = 256, N = R * R;
   constexpr int GPB = NT / R;          // 8 rows per row block
   constexpr int WPR = N / 32;          // 32 mask words per row = one per lane
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256, 3) void k_rowfwd32(const JobDesc* jobs,
   const int npair = pair_step ? 1 : P / 2;   // plane-cached step: only the flipped plane's pair
   const int j = bid / npair;
   const JobDesc jb = first_pass_job(jobs, actions, err, j, rbw == 0 && bid % npair == 0, (int64_t)N * N, P, CH);
-  if (jb.env < 0) return;  // uniform per block
+  if (jb.env < 0 || (phase && phase[j])) return;  // uniform per block (a walk slot whose A / B are kept)
   const int q = pair_step ? (jb.flip_plane >> 1) : bid % npair;
   const int pa = 2 * q, pb = 2 * q + 1;
   const uint32_t* plane_a = mask + ((size_t)jb.env * CH + jb.group * P + pa) * N * WPR;
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
                                                  float2* __restrict__ ws_b,
                                                  const float2* __restrict__ htab,
                                                  const float2* __restrict__ tw_glob, int P,
-                                                 int pair_step) {
+                                                 int pair_step, const uint8_t* __restrict__ phase) {
   constexpr int N = R * R;
   constexpr int GPB = 256 / R;          // lane groups (= input lines) per block iteration
   constexpr int LB = (N / 2) / (GPB * ITER);
@@ -476,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
   const int np = pair_step ? 2 : P;     // plane-cached step: the flipped plane's pair only
   const int j = bid / np;
   const JobDesc jb = jobs[j];
-  if (jb.env < 0) return;
+  if (jb.env < 0 || (phase && phase[j])) return;   // (a walk slot whose B is kept)
   const int p = pair_step ? (jb.flip_plane & ~1) + bid % 2 : bid % np;
   using PA = LayoutA<R>;   // A planes: N/2 lines
   using PB = LayoutB<R>;   // B planes: N lines
@@ -713,6 +715,12 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
   const int rb = bid % RB;
   const int j = bid / RB;
   const JobDesc jb = jobs[j];
+  if constexpr (WALK) {
+    if (wk.phase && wk.phase[j] == 2) {   // (r06) a kept walk slot: its partials and fresh pair stand
+      walk_planes_arrive(wk, reinterpret_cast<char*>(scratch));
+      return;
+    }
+  }
   if (jb.env < 0) {
     if (threadIdx.x == 0) {
       double* o = partial + ((size_t)j * RB + rb) * 3;
@@ -1088,20 +1096,20 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if constexpr (R == 32) {
       if (small)
         hipLaunchKernelGGL((k_rowfwd32<SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(256), 0, st, jobs, mask,
-                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err, pd.walk_phase);
       else
         hipLaunchKernelGGL((k_rowfwd32<SK>), dim3(rf_blocks), dim3(256), 0, st, jobs, mask, pd.ws_a, pd.tw, P, CH,
-                           pd.va, pd.vb, pair, pd.actions, pd.act_err);
+                           pd.va, pd.vb, pair, pd.actions, pd.act_err, pd.walk_phase);
     } else if constexpr (kTiledB<R>) {
       if (small)
         hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK, 1>), dim3(rf_blocks * rowfwd_iters<R>()), dim3(kRowNT<R>), 0,
-                           st, jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
+                           st, jobs, mask, pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err, pd.walk_phase);
       else
         hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask,
-                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
+                           pd.ws_a, pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err, pd.walk_phase);
     } else {
       hipLaunchKernelGGL((k_rowfwd<R, kRowNT<R>, SK>), dim3(rf_blocks), dim3(kRowNT<R>), 0, st, jobs, mask, pd.ws_a,
-                         pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err);
+                         pd.tw, P, CH, pd.va, pd.vb, pair, pd.actions, pd.act_err, pd.walk_phase);
     }
     if (tm) tm->end(0, n_jobs, st);
   }
@@ -1110,13 +1118,13 @@ static hipError_t launch_passes(const PlanDev& pd, const JobDesc* jobs, int n_jo
     if constexpr (kTiledB<R>) {
       if (small)
         hipLaunchKernelGGL((k_col2<R, SK, 1>), dim3(col_blocks * col2_iters<R>()), dim3(256), 0, st, jobs, pd.ws_a,
-                           pd.ws_b, pd.htab, pd.tw, P, pair);
+                           pd.ws_b, pd.htab, pd.tw, P, pair, pd.walk_phase);
       else
         hipLaunchKernelGGL((k_col2<R, SK>), dim3(col_blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
-                           pd.tw, P, pair);
+                           pd.tw, P, pair, pd.walk_phase);
     } else {
       hipLaunchKernelGGL((k_col2<R, SK>), dim3(col_blocks), dim3(256), 0, st, jobs, pd.ws_a, pd.ws_b, pd.htab,
-                         pd.tw, P, pair);
+                         pd.tw, P, pair, pd.walk_phase);
     }
     if (tm) tm->end(1, n_jobs, st);
   }

@@ -19,7 +19,7 @@ constexpr int kFillRejected = -2;            // job of a candidate the on-pixel 
 // LDS the decision needs for RB row blocks per job (carved out of a caller's buffer)
 __host__ __device__ constexpr size_t walk_planes_lds_bytes(int RB) {
   return (size_t)kWalkPlanesCJ * 3 * RB * 8 + 256 * 3 * 8 + 256 * sizeof(JobDesc) + 256 * 8 + 256 * 4 * 4 +
-         512 * 8 + 3 * HBX_MAX_GROUPS * 8 + 128 + HBX_MAX_GROUPS * 8;
+         512 * 8 + 3 * HBX_MAX_GROUPS * 8 + 128 + HBX_MAX_GROUPS * 8 + 16;
 }
 
 // (ABI v13, extension -- no reference counterpart) the on-pixel ratio constraint: a
@@ -70,9 +70,10 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
   int64_t* s_order = reinterpret_cast<int64_t*>(carve(512 * 8));
   double* s_base = reinterpret_cast<double*>(carve(3 * HBX_MAX_GROUPS * 8));
   int64_t* s_i64 = reinterpret_cast<int64_t*>(carve(3 * 8));           // pos, total, acc
-  int* s_int = reinterpret_cast<int*>(carve(2 * 4));                    // done, stop_en
+  int* s_int = reinterpret_cast<int*>(carve(4 * 4));                    // done, stop_en, ring, -
   double* s_dbl = reinterpret_cast<double*>(carve(4 * 8));              // prev, last, init, stop_diff
   int64_t* s_fill = reinterpret_cast<int64_t*>(carve(HBX_MAX_GROUPS * 8));   // on-pixel counts (fill on)
+  uint64_t* s_tpair = reinterpret_cast<uint64_t*>(carve(8));            // (group, pair)s this batch accepted into
   hbx_dbs_walk_t* w = a.w;
   const int k = threadIdx.x;
   const int64_t hw = (int64_t)H * W;
@@ -104,10 +105,15 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
       }
     }
   }
+  // (r06) retention: candidate i of the batch sits in job slot (ring + i) % K; a call's first batch
+  // (decide = 0) starts at ring 0 with every slot propagated in full
+  const bool keep = a.phase != nullptr && a.ring != nullptr;
   if (k == 0) {
     s_i64[0] = pos0; s_i64[1] = total0; s_i64[2] = w->accepted; s_int[0] = w->done;
     s_int[1] = w->stop_enabled; s_dbl[0] = w->prev_psnr; s_dbl[1] = w->last_psnr;
     s_dbl[2] = w->init_psnr; s_dbl[3] = w->stop_diff;
+    s_int[2] = (keep && decide) ? *a.ring : 0;
+    s_tpair[0] = 0;
   }
   for (int i = k; i < 2 * K; i += blockDim.x) s_order[i] = (pos0 + i < total0) ? a.order[pos0 + i] : -1;
   if (decide && k < K) {
@@ -164,15 +170,18 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
   if (k == 0 && decide && !s_int[0]) {
     const int64_t pos = s_i64[0];
     const int nk = (int)min((int64_t)K, s_i64[1] - pos);
+    const int ring = s_int[2];
     double prev = s_dbl[0], last = s_dbl[1];
     int64_t acc_n = s_i64[2];
     unsigned touched = 0;
+    uint64_t tpair = 0;
     int visited = nk, done = 0;
-    for (int c = 0; c < nk; ++c) {
+    for (int i = 0; i < nk; ++i) {
+      const int c = (ring + i) % K;         // candidate i's job slot
       const JobDesc jb = s_job[c];
       // (an inadmissible candidate, env == kFillRejected, was judged against the batch's starting
       // count: it ends the batch like any other candidate of a touched group)
-      if (jb.env != -1 && ((touched >> jb.group) & 1u)) { visited = c; break; }
+      if (jb.env != -1 && ((touched >> jb.group) & 1u)) { visited = i; break; }
       double ps = NAN;
       const double* js = s_js + 3 * c;
       if (jb.env >= 0) {
@@ -205,18 +214,20 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
           s_fill[jb.group] = f;
           a.fill_count[jb.group] = f;
         }
-        if (acc_n < a.accept_cap) { a.accept_pos[acc_n] = pos + c; a.accept_psnr[acc_n] = ps; }
+        if (acc_n < a.accept_cap) { a.accept_pos[acc_n] = pos + i; a.accept_psnr[acc_n] = ps; }
         ++acc_n;
         prev = ps;
         touched |= 1u << jb.group;
+        tpair |= 1ull << ((jb.group * P + jb.flip_plane) >> 1);
         if (s_int[1] && ps - s_dbl[2] >= s_dbl[3]) {   // DBS_ratio_0.5.py:366-372
           done = 1;
           w->stopped_early = 1;
-          visited = c + 1;
+          visited = i + 1;
           break;
         }
       }
     }
+    s_tpair[0] = tpair | ((uint64_t)touched << 48);   // pairs (bits < 48) and groups
     w->accepted = acc_n;
     w->prev_psnr = prev;
     w->last_psnr = last;
@@ -233,6 +244,9 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
   if (k < K) {                              // the next batch's jobs
     const int off = (int)s_i64[2];
     const int64_t qq = s_i64[0] + off + k;
+    // candidate k of the next batch: job slot (ring + off + k) % K with retention (the slot the
+    // same candidate had in this batch when k < K - off), slot k without
+    const int slot = keep ? (s_int[2] + off + k) % K : k;
     JobDesc jd;
     jd.env = -1; jd.group = 0; jd.flip_plane = -1; jd.flip_pix = 0;
     if (!s_int[0] && qq < s_i64[1]) {
@@ -252,8 +266,22 @@ __device__ __forceinline__ void walk_planes_decide(const WalkPlanesArgs& a, int 
         }
       }
     }
-    a.jobs[k] = jd;
+    if (keep) {
+      // what the slot still needs: a candidate this batch propagated (same slot, k < K - off) keeps
+      // its pair's B unless an accept of this batch changed that pair's mask, and keeps its
+      // partials and fresh pair too unless an accept changed its colour group's cached planes
+      uint8_t ph = 0;
+      const JobDesc old = s_job[slot];
+      if (decide && off > 0 && k < K - off && jd.env >= 0 && old.env >= 0) {
+        const uint64_t tp = s_tpair[0];
+        if (!((tp >> ((jd.group * P + jd.flip_plane) >> 1)) & 1ull))
+          ph = ((tp >> (48 + jd.group)) & 1ull) ? 1 : 2;
+      }
+      a.phase[slot] = ph;
+    }
+    a.jobs[slot] = jd;
   }
+  if (keep && k == 0) *a.ring = decide ? (s_int[2] + (int)s_i64[2]) % K : 0;
 }
 
 // The fused decision's hand-off, at the end of every k_rowinv_d workgroup of a walk batch: this
