@@ -602,13 +602,14 @@ __global__ __launch_bounds__(256, 2) void k_col2(const JobDesc* __restrict__ job
 // ---------------------------------------------------------------------------
 // k_rowinv's tail: plane mean, f64 partials of (I*T, I^2, T^2) against the target row,
 // fixed-order reduction over the group's lanes and the block's rows.
-template <int R, int GPB, bool SC1 = false>
+template <int R, int GPB, bool SC1 = false, bool TPRE = false>
 __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, const JobDesc& jb, int j, int y,
                                                 int rb, int grp, int t, const float* __restrict__ target,
                                                 size_t tmask, float* __restrict__ inten_out, int inten_by_env,
                                                 double* __restrict__ partial, double (&red)[GPB][3],
                                                 const int32_t* __restrict__ rc_pending = nullptr,
-                                                float* __restrict__ rc_cache = nullptr) {
+                                                float* __restrict__ rc_cache = nullptr,
+                                                const float* tpre = nullptr) {
   constexpr int N = R * R;
   constexpr int RB = N / GPB;
   const float invp = 1.0f / (float)P;
@@ -619,7 +620,7 @@ __device__ __forceinline__ void rowinv_epilogue(float (&acc)[R], int P, int G, c
 #pragma unroll
   for (int k = 0; k < R; ++k) {
     const float I = acc[k] * invp;
-    const float T = trow[t + R * k];
+    const float T = TPRE ? tpre[k] : trow[t + R * k];   // TPRE: the caller loaded the row ahead
     sxy = fma((double)I, (double)T, sxy);
     sxx = fma((double)I, (double)I, sxx);
     syy = fma((double)T, (double)T, syy);
@@ -836,6 +837,22 @@ __global__ __launch_bounds__(256, 2) void k_rowinv_d(const JobDesc* __restrict__
       load_plane(va, p + 2 < P ? p + 2 : p + 1);
       finish_plane(vb, p + 1);
     }
+  } else if constexpr (LEAN) {
+    // (r06) the last plane peeled: its FFT runs with the target row's loads in flight instead of a
+    // re-read of plane P - 1 (the loads the tail waited for; 32 more VGPRs fit the lean kernel)
+#pragma unroll 1
+    for (int p = 0; p < P - 1; ++p) {
+      finish_plane(va, p);
+      load_plane(va, p + 1);
+    }
+    const float* trow = target + ((((size_t)jb.env * G + jb.group) * N + y) * N & tmask);
+    float tv[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) tv[k] = trow[t + R * k];
+    finish_plane(va, P - 1);
+    rowinv_epilogue<R, GPB, false, true>(acc, P, G, jb, j, y, rb, grp, t, target, tmask, inten_out, inten_by_env,
+                                         partial, red, rc_pending, rc_cache, tv);
+    return;
   } else {
 #pragma unroll 1
     for (int p = 0; p < P; ++p) {
