@@ -174,60 +174,3 @@ def check(rc: int, where: str):
         msg = load().hbx_last_error().decode(errors="replace")
         raise HbxError(rc, where, msg)
 
-
-_hip_rt = None
-
-
-def _hip():
-    """The HIP runtime this process already runs (torch's and libhbx's: one soname, loaded once)."""
-    global _hip_rt
-    with _lock:
-        if _hip_rt is None:
-            rt = C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)
-            rt.hipEventCreateWithFlags.argtypes = [C.POINTER(VP), C.c_uint]
-            rt.hipEventRecord.argtypes = [VP, VP]
-            rt.hipEventSynchronize.argtypes = [VP]
-            rt.hipEventQuery.argtypes = [VP]
-            rt.hipEventDestroy.argtypes = [VP]
-            for f in (rt.hipEventCreateWithFlags, rt.hipEventRecord, rt.hipEventSynchronize, rt.hipEventQuery,
-                      rt.hipEventDestroy):
-                f.restype = C.c_int
-            _hip_rt = rt
-    return _hip_rt
-
-
-class HipEvent:
-    """A timing-free HIP event recorded on a raw stream handle: the per-step readback wait of the
-    envs.  torch.cuda.Event.record() looks up torch's current stream in Python on every call
-    (~5-10 us per SB3 step, tools/step_prof.py); this records on the handle the step's launches
-    used and waits the same way (hipEventSynchronize, flags as torch's default event)."""
-
-    _DISABLE_TIMING = 0x2
-
-    def __init__(self):
-        self._rt = _hip()
-        self._h = VP()
-        rc = self._rt.hipEventCreateWithFlags(C.byref(self._h), self._DISABLE_TIMING)
-        if rc != 0:
-            raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
-
-    def record(self, stream: int):
-        rc = self._rt.hipEventRecord(self._h, stream)
-        if rc != 0:
-            raise RuntimeError(f"hipEventRecord failed ({rc})")
-
-    def synchronize(self):
-        rc = self._rt.hipEventSynchronize(self._h)
-        if rc != 0:
-            raise RuntimeError(f"hipEventSynchronize failed ({rc})")
-
-    def query(self) -> bool:
-        return self._rt.hipEventQuery(self._h) == 0   # hipErrorNotReady (600) while pending
-
-    def __del__(self):
-        h, rt = getattr(self, "_h", None), getattr(self, "_rt", None)
-        if h and h.value and rt is not None:
-            try:
-                rt.hipEventDestroy(h)
-            except Exception:  # noqa: BLE001 -- interpreter shutdown
-                pass

@@ -514,7 +514,7 @@ class HologramVecEnv(_VecEnvBase):
         self._arow = HostRow(self.plan.lib, 8 * max(n, 1))
         self._act_np = self._arow.array.view(np.int64)[:n]
         self._dev_index = self.device.index if self.device.type == "cuda" else None
-        self._readback = _lib.HipEvent() if self.device.type == "cuda" else None   # recorded on the raw stream
+        self._readback = torch.cuda.Event() if self.device.type == "cuda" else None
         self._actions = None
         self._fast_args = None
         self._fast_ids = None
@@ -926,7 +926,7 @@ class HologramVecEnv(_VecEnvBase):
             m.queue_recon()                       # recon_image D2H behind the step, before the wait
         # the observation views and infos are built while the step is in flight
         if self._readback is not None:
-            self._readback.record(_raw_stream(self._dev_index))
+            self._readback.record()
             if self.state.recon is not None and self.mode != "psf" and self.cfg.groups > 1:
                 self._settle()                    # (ABI v12: nothing is pending at one group)
         obs = self.observe(stepped=True)
@@ -1372,7 +1372,7 @@ class BinaryHologramEnv(spaces.EnvBase):
             vec._host_t.copy_(vec._out_raw, non_blocking=True)
         recon = torch.empty(self._recon_shape, dtype=torch.float32, pin_memory=True)
         recon.copy_(vec.state.recon[0:1], non_blocking=True)   # env.py:179, queued behind the step
-        vec._readback.record(_raw_stream(vec._dev_index))
+        vec._readback.record()
         if self.cfg.groups > 1:
             vec._settle()
         vec._readback.synchronize()

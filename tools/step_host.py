@@ -45,7 +45,7 @@ def main():
         t1 = ns()
         obs = vec.observe(stepped=True)
         infos = [{} for _ in range(B)]
-        ev.record(torch._C._cuda_getCurrentRawStream(vec._dev_index))
+        ev.record()
         vec._settle()
         t2 = ns()
         q = 0
