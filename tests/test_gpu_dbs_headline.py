@@ -215,6 +215,32 @@ def test_fft_greedy_plane_cache_equals_full_repropagation(golden_dir, name, stop
     assert len(full.accepted_positions) > 100
 
 
+@pytest.mark.parametrize("k", [2, 4, 7])
+def test_fft_walk_retention_equals_fresh_batches(golden_dir, monkeypatch, k):
+    """(r06) the device walk keeps the candidates a batch propagated but did not visit (their job
+    slot, B and -- untouched colour group -- partials) for the next batch.  The walk with that on
+    and with it off (HBX_WALK_NO_RETAIN, every batch propagated from scratch) makes the same
+    decisions with the same PSNR bits and leaves the same mask, at fixed speculation depths."""
+    from hbx import dbs
+    d, ocfg, pre, tgt, order = _fixture(golden_dir, "dbs_prefix_1024x24_16k.npz")
+    runs = {}
+    for retain in (True, False):
+        if retain:
+            monkeypatch.delenv("HBX_WALK_NO_RETAIN", raising=False)
+        else:
+            monkeypatch.setenv("HBX_WALK_NO_RETAIN", "1")
+        plan, mask, target = _dev(ocfg, pre, tgt)
+        res = dbs.greedy(plan, mask, target, order[:3000], mode="fft", k_min=k, k_max=k)
+        runs[retain] = (res, mask.cpu().numpy())
+        plan.close()
+    (a, ma), (b, mb) = runs[True], runs[False]
+    assert a.accepted_positions == b.accepted_positions
+    assert a.accepted_psnr == b.accepted_psnr                       # bit for bit
+    assert a.final_psnr == b.final_psnr and a.steps == b.steps and a.launches == b.launches
+    assert np.array_equal(ma, mb)
+    assert len(a.accepted_positions) > 100
+
+
 def test_fft_walk_edge_orders(golden_dir):
     """The device-decided FFT-mode walk (hbx_dbs_walk_planes) on the orders that stress its batch
     logic, each against the host-decided full re-propagation (planes=False): an empty order, one
