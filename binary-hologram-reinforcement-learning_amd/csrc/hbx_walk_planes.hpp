@@ -53,7 +53,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t walk_planes_rsrc(const void* b
 // serial loop's bit for bit; the batch ends before the first candidate of a touched group (it
 // needs a fresh propagation) -- up to G accepts per batch.  Then -- decide = 0 too -- the NEXT
 // batch's K jobs are written from the walk state (invalid jobs once the walk is done, so the
-// passes behind return at once).  SC1: the partials come from other workgroups of the SAME launch
+// passes behind return at once).  (r06) With a ring / phase buffer (the fused walk), candidate i of
+// a batch sits in job slot (ring + i) % K: the candidates this batch propagated but did not visit
+// stay in their slots as the next batch's first candidates, and phase[slot] tells the passes what
+// they still need (0 all, 1 only k_rowinv_d, 2 nothing; see WalkPlanesArgs).  SC1: the partials come from other workgroups of the SAME launch
 // (the fused decision), written through with sc1 stores -- read them with sc1 loads, which miss
 // this XCD's L2.
 template <bool SC1>
