@@ -24,6 +24,14 @@ total = 24 * 1024 * 1024
 n = int(sys.argv[1]) if len(sys.argv) > 1 and int(sys.argv[1]) > 0 else total
 mode = sys.argv[2] if len(sys.argv) > 2 else "psf"
 assert mode in ("psf", "fft")
+# optional 3rd argument "ktable=r06": the FFT walk's K policy from the r06 batch times with candidate
+# retention (tools/dbs_walk_bench.py --k at q ~ 0.5, profiles/r06/walk_retain_r06af/) instead of r05's
+KTABLE = sys.argv[3].split("=", 1)[1] if len(sys.argv) > 3 and sys.argv[3].startswith("ktable=") else "r05"
+if KTABLE == "r06":
+    _orig_k = dbs.walk_k_planes
+    _r06 = {1: 45.0, 2: 56.4, 3: 72.3, 4: 78.4, 5: 91.8, 6: 98.3, 7: 104.4, 8: 110.4}
+    dbs.walk_k_planes = lambda q, groups=3, k_min=1, k_max=64, table=None, slope=11.7: _orig_k(
+        q, groups, k_min, k_max, table=_r06, slope=6.9)
 cfg = hbx.rgb_config(1024)
 g = torch.Generator(device="cuda").manual_seed(0)
 pre = torch.rand((24, 1024, 1024), generator=g, device="cuda")
@@ -58,4 +66,5 @@ print(json.dumps({
     "mode": ("device-resident walk (hbx_dbs_walk_psf), exact refresh every 4096 accepts" if mode == "psf" else
              "FFT mode (f32 re-propagation per candidate, the reference's algorithm) on the plane cache, "
              "device-decided batches (hbx_dbs_walk_planes)"),
+    "k_policy": KTABLE,
     "data": "synthetic seeded U[0,1) pre-model (threshold 0.5) and target"}))
